@@ -1,0 +1,109 @@
+"""CPU: pin the oracle (CPU restatement) against fixtures recorded from the imported reference."""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import body_post, hand_post, network
+from oracle.cv_resize import cubic_coeffs, resize_cubic
+
+from conftest import GOLDEN
+
+
+def _files(pat):
+    fs = sorted(glob.glob(os.path.join(GOLDEN, pat)))
+    assert fs, pat
+    return fs
+
+
+@pytest.mark.parametrize("path", _files("net_*.npz"), ids=os.path.basename)
+def test_network_matches_reference_model(path):
+    d = np.load(path)
+    net = "body" if "body" in os.path.basename(path) else "hand"
+    sd = network.seeded_state_dict(net, 0)
+    x = torch.from_numpy(d["x"])
+    if net == "body":
+        paf, heat = network.body_forward(x, sd)
+        np.testing.assert_allclose(paf.numpy(), d["paf"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(heat.numpy(), d["heat"], rtol=1e-5, atol=1e-6)
+        assert (heat.numpy() >= 0).all()   # ReLU after Mconv7_stage6_L2 (src/model.py:30-33)
+    else:
+        np.testing.assert_allclose(network.hand_forward(x, sd).numpy(), d["heat"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("path", _files("body_planted_*.npz"), ids=os.path.basename)
+def test_body_post_matches_reference(path):
+    d = np.load(path)
+    lowres = [(d["paf"], d["heat"], list(d["pad"]), tuple(d["padded_hw"]))]
+    if str(d["error"]):
+        with pytest.raises(IndexError):
+            body_post.post_from_lowres(tuple(d["img_hw"]), lowres)
+        return
+    cand, subset = body_post.post_from_lowres(tuple(d["img_hw"]), lowres)
+    assert cand.shape == d["candidate"].shape and cand.dtype == d["candidate"].dtype
+    assert np.array_equal(cand, d["candidate"])
+    assert np.array_equal(subset, d["subset"])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("path", _files("body_e2e_*.npz"), ids=os.path.basename)
+def test_body_end_to_end_matches_reference(path):
+    d = np.load(path)
+    sd = network.seeded_state_dict("body", 0)
+
+    def net_fn(x):
+        p, h = network.body_forward(torch.from_numpy(x), sd)
+        return p.numpy(), h.numpy()
+
+    cand, subset = body_post.body_infer(d["img"], net_fn)
+    assert np.array_equal(cand, d["candidate"])
+    assert np.array_equal(subset, d["subset"])
+
+
+@pytest.mark.parametrize("path", _files("hand_planted_*.npz"), ids=os.path.basename)
+def test_hand_post_matches_reference(path):
+    d = np.load(path)
+    size = int(d["size"])
+    calls = iter([d[f"heat{i}"] for i in range(4)])
+    peaks = hand_post.hand_infer(np.zeros((size, size, 3), np.uint8), lambda x: next(calls)[None])
+    assert peaks.dtype == d["peaks"].dtype
+    assert np.array_equal(peaks, d["peaks"])
+
+
+def test_hand_output_size_table():
+    """Known-answer artefact shipped by the reference (src/hand_model_output_size.json)."""
+    with open(os.path.join(GOLDEN, "hand_model_output_size.json")) as f:
+        table = {int(k): v for k, v in json.load(f).items()}
+    assert len(table) == 990
+    for i, v in table.items():
+        assert v == i // 2 // 2 // 2   # three floor-mode 2x2 pools (src/model.py:147,150,155)
+
+
+def test_cubic_coeffs_partition_of_unity():
+    f = np.linspace(0, 1, 257, dtype=np.float32)[:-1]
+    c = cubic_coeffs(f)
+    assert np.allclose(c.sum(1), 1, atol=1e-6)
+    assert np.array_equal(cubic_coeffs(np.float32([0]))[0], np.float32([0, 1, 0, 0]))
+
+
+def test_resize_identity_and_sizes():
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, (37, 53, 3), dtype=np.uint8)
+    assert np.array_equal(resize_cubic(img, (53, 37)), img)
+    out = resize_cubic(img, (0, 0), fx=0.5, fy=0.5)
+    assert out.shape == (round(37 * 0.5), round(53 * 0.5), 3)
+    f = rng.random((5, 7, 19), dtype=np.float32)
+    up = resize_cubic(f, (0, 0), fx=8, fy=8)
+    assert up.shape == (40, 56, 19) and up.dtype == np.float32
+    # a constant map stays constant through the cubic kernel (coefficients sum to ~1)
+    c = np.full((5, 7, 2), 0.25, np.float32)
+    assert np.allclose(resize_cubic(c, (0, 0), fx=8, fy=8), 0.25, atol=1e-6)
+
+
+def test_flops_match_survey():
+    assert network.body_flops(184, 328) == 121158571264
+    assert network.body_flops(184, 184) == 67967003392
+    assert network.hand_flops(368, 368) == 206375342080
