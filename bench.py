@@ -1,0 +1,189 @@
+"""Benchmark: Body() frames/s at 368x656 (BASELINE.json metric), 1..8 MI355X, one process per GPU.
+
+Workload (a "step"): one video batch of B synthetic 368x656 uint8 BGR frames per GPU, already
+resident in HBM, through the full Body() path on the GPU — uint8 cubic resize/pad/normalise,
+the 92-conv VGG-19/CPM network, x8 cubic upsample + resize, Gaussian peak NMS, PAF scoring,
+greedy matching, person assembly — producing one fixed-size keypoint record per frame; with
+N > 1 ranks the records are gathered across ranks with RCCL (all_gather over xGMI) each step.
+Frames shard across ranks (weak scaling: B frames per GPU).  Weights are seeded synthetic
+(real .pth files are unavailable offline).
+
+Prints ONE JSON line on rank 0 (driver contract) including:
+* roofline: the 7x7-conv kernel class (68 % of network FLOPs), algorithmic FLOPs per launch
+  / mean launch time from HIP events recorded on the library's stream inside the timed region;
+* cpu_baseline: the oracle (torch-CPU conv graph + NumPy/SciPy post-processing, proven
+  identical to the reference on the golden fixtures) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "pytorch-openpose_amd")
+for p in (PKG, REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+H, W = 368, 656
+PEAK_FP32_TFLOPS = 157.3  # MI355X fp32 matrix peak (MI355X_MICROARCH.md: spec 157.3, 155 measured)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--latency-iters", type=int, default=10)
+    return ap.parse_args()
+
+
+def cpu_baseline(frames_np, seconds):
+    """Oracle (test infrastructure, used only as the timed CPU baseline) on whole frames."""
+    from oracle import body_post, network
+    from src.weights import BENCH_OUT_SCALE
+    threads = os.cpu_count() or 1
+    torch.set_num_threads(threads)
+    sd = network.seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE)
+
+    def net_fn(x):
+        p, h = network.body_forward(torch.from_numpy(x), sd)
+        return p.numpy(), h.numpy()
+
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        body_post.body_infer(frames_np[n % len(frames_np)], net_fn)
+        n += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} frame(s) of 368x656 through oracle Body() (torch-CPU net + NumPy/SciPy post), "
+                      f"{dt:.1f} s, torch threads={threads}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from src.body import Body
+    from src.weights import BENCH_OUT_SCALE, seeded_state_dict
+
+    body = Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE), device=local)
+    B = args.batch
+    rng = np.random.default_rng(1 + rank)
+    frames_np = rng.integers(0, 256, (B, H, W, 3), dtype=np.uint8)
+    frames = torch.from_numpy(frames_np).to(dev)
+    rb = body.handle.record_bytes()
+    rec = torch.empty((B, rb), dtype=torch.uint8, device=dev)
+    gathered = torch.empty((world * B, rb), dtype=torch.uint8, device=dev) if world > 1 else None
+    lib_stream = torch.cuda.ExternalStream(body.handle.stream(), device=dev)
+
+    def step():
+        body.infer_records(frames, rec)
+        if world > 1:
+            with torch.cuda.stream(lib_stream):
+                torch.distributed.all_gather_into_tensor(gathered, rec)
+
+    for _ in range(args.warmup):
+        step()
+    body.handle.synchronize()
+    torch.cuda.synchronize()
+    # sanity on the warm output (outside the timed region)
+    statuses = rec.view(torch.int32)[:, 0].cpu().numpy()
+    counts = rec.view(torch.int32)[:, 1:3].cpu().numpy()
+
+    body.handle.profile(True)
+    body.handle.profile_reset()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    body.handle.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    prof = body.handle.profile_read()
+    body.handle.profile(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # single-frame latency (C2: one frame, host in -> host out through Body.__call__)
+    lat = []
+    if rank == 0 and args.latency_iters > 0:
+        one = frames_np[0]
+        body(one)
+        for _ in range(args.latency_iters):
+            t1 = time.perf_counter()
+            body(one)
+            lat.append(time.perf_counter() - t1)
+
+    if rank == 0:
+        frames_total = world * B * args.steps
+        c7 = prof.get("conv7x7", {"count": 0, "ms": 0.0, "flops": 0.0})
+        conv_all = {k: v for k, v in prof.items() if k.startswith("conv")}
+        achieved = (c7["flops"] / (c7["ms"] * 1e-3) / 1e12) if c7["ms"] > 0 else 0.0
+        stage_ms = {k: round(v["ms"] / args.steps, 4) for k, v in sorted(prof.items())}
+        net_flops = sum(v["flops"] for v in conv_all.values())
+        net_ms = sum(v["ms"] for v in conv_all.values())
+        out = {
+            "metric": "frames/sec (body+PAF grouping) at 368x656",
+            "value": frames_total / dt,
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (uniform uint8 frames, seeded He-normal weights; real weights unavailable offline)",
+            "config": {"workload": f"C2/C4: Body() on 368x656 frames, {B} frames per GPU per step, "
+                                   f"RCCL all_gather of per-frame keypoint records when n_gpus > 1",
+                       "frame": [H, W], "frames_per_gpu_per_step": B, "scale_search": [0.5],
+                       "net_input": [184, 328], "parallelism": f"frame-sharded dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": "conv_igemm_f32 (7x7 CPM stages)",
+                         "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_FP32_TFLOPS,
+                         "per_launch_flops": c7["flops"] / max(1, c7["count"]),
+                         "mean_launch_ms": c7["ms"] / max(1, c7["count"]), "traffic": None},
+            "network_tflops": net_flops / (net_ms * 1e-3) / 1e12 if net_ms > 0 else 0.0,
+            "stage_ms_per_step": stage_ms,
+            "latency_ms_single_frame": (float(np.median(lat)) * 1e3) if lat else None,
+            "frames_status_nonzero": int((statuses != 0).sum()),
+            "mean_peaks_per_frame": float(counts[:, 0].mean()),
+            "mean_people_per_frame": float(counts[:, 1].mean()),
+        }
+        if not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(frames_np[:2], args.cpu_seconds)
+        print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

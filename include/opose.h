@@ -1,0 +1,154 @@
+/*
+ * opose.h — C ABI of libopose.so, the MI355X-native OpenPose Body/Hand inference path.
+ *
+ * Drop-in boundary for hitmaxiang/pytorch-openpose `src/` (pure Python in the reference;
+ * these entry points are what a ctypes/cffi binding of that path binds — see INTEGRATION.md):
+ *
+ *   reference interface (file:line)                         replaced by
+ *   ------------------------------------------------------  -----------------------------------
+ *   Body.__init__ / Hand.__init__  src/body.py:16-22,        opose_create + opose_load_weights
+ *                                  src/hand.py:17-23
+ *   util.transfer                  src/util.py:36-40         key mapping done by the caller; tensors
+ *                                                            passed in reference state_dict order
+ *   bodypose_model.forward         src/model.py:106-133      opose_body_forward
+ *   handpose_model.forward         src/model.py:197-214      opose_hand_forward
+ *   Body.__call__                  src/body.py:24-212        opose_body_infer
+ *   Body.__call__ after the net    src/body.py:52-212        opose_body_post   (parity entry point)
+ *   Hand.__call__                  src/hand.py:25-75         opose_hand_infer
+ *   Hand.__call__ after the net    src/hand.py:51-75         opose_hand_post   (parity entry point)
+ *
+ * Conventions: plain pointers and sizes only; 0 = OK, negative = error (see opose_status).
+ * Host pointers are caller-owned and read-only; the library copies them. A handle owns one
+ * device, one HIP stream (or the caller's, see opose_set_stream), its weights and workspace.
+ * Calls on one handle must be serialised by the caller; handles are independent.
+ */
+#ifndef OPOSE_H
+#define OPOSE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct opose_ctx opose_t;
+
+typedef enum opose_status {
+    OPOSE_OK = 0,
+    OPOSE_E_ARG = -1,        /* bad argument / null pointer                         */
+    OPOSE_E_SHAPE = -2,      /* unsupported shape                                   */
+    OPOSE_E_HIP = -3,        /* HIP runtime error (message in opose_last_error)     */
+    OPOSE_E_WEIGHTS = -4,    /* weights missing or of the wrong shape               */
+    OPOSE_E_CAPACITY = -5,   /* a per-frame record overflowed (peaks/people)        */
+    OPOSE_E_ASSEMBLY = -6,   /* reference IndexError: a 3rd subset row matched a
+                                connection (src/body.py:170-173)                    */
+} opose_status;
+
+enum { OPOSE_NET_BODY = 0, OPOSE_NET_HAND = 1 };
+
+/* flags for *_infer / *_post / *_forward */
+enum {
+    OPOSE_IN_DEVICE = 1,     /* input pointer is device memory                      */
+    OPOSE_OUT_DEVICE = 2,    /* output pointer is device memory; call is async on the
+                                handle's stream                                     */
+};
+
+#define OPOSE_MAX_SCALES 8
+
+/* Hard-coded locals of the reference, exposed with the reference defaults
+ * (src/body.py:25-31, src/hand.py:26-31). */
+typedef struct opose_params {
+    int n_scales;
+    double scales[OPOSE_MAX_SCALES]; /* scale_search; Body default {0.5}, Hand {0.5,1,1.5,2} */
+    double boxsize;                  /* 368  */
+    int stride;                      /* 8    */
+    int pad_value;                   /* 128  */
+    double thre1;                    /* 0.1  body peak threshold                  */
+    double thre2;                    /* 0.05 PAF sample threshold                 */
+    double thre_hand;                /* 0.03 hand component threshold             */
+} opose_params;
+
+void opose_default_params(int net, opose_params* p);
+
+/* ---- lifetime ---------------------------------------------------------------------- */
+int opose_create(int device, opose_t** out);
+void opose_destroy(opose_t* h);
+const char* opose_last_error(const opose_t* h);
+int opose_set_stream(opose_t* h, void* hip_stream);   /* NULL = the handle's own stream */
+void* opose_get_stream(const opose_t* h);
+int opose_synchronize(opose_t* h);
+
+/* Capacity of one Body record: peaks kept per part and people kept per frame.
+ * Defaults 96 / 96.  Overflow makes the frame's status OPOSE_E_CAPACITY. */
+int opose_set_capacity(opose_t* h, int peaks_per_part, int max_people);
+
+/* Per-frame Body record (fixed size, the unit of the multi-GPU gather):
+ *   int32  status, n_cand, n_people, reserved
+ *   double candidate[18*peaks_per_part][4]    x, y, score, id  (src/body.py:160,211)
+ *   double subset[max_people][20]             ids (-1) | total score | part count */
+size_t opose_body_record_bytes(const opose_t* h);
+
+/* ---- weights ------------------------------------------------------------------------ */
+/* tensors[i] = host fp32 data of the i-th state_dict tensor in reference order
+ * (weight, bias per conv; OIHW); shapes = n x 4 int64 (bias: {C,1,1,1}). */
+int opose_load_weights(opose_t* h, int net, const float* const* tensors,
+                       const int64_t* shapes, int n);
+
+/* ---- network only (src/model.py forward) ------------------------------------------- */
+/* x [N,3,Hp,Wp] fp32 NCHW (Hp, Wp multiples of 8); paf [N,38,Hp/8,Wp/8], heat [N,19,..] */
+int opose_body_forward(opose_t* h, const float* x, int N, int Hp, int Wp,
+                       float* paf, float* heat, int flags);
+/* heat [N,22,Hp/8,Wp/8] */
+int opose_hand_forward(opose_t* h, const float* x, int N, int Hp, int Wp, float* heat, int flags);
+
+/* ---- end to end ---------------------------------------------------------------------- */
+/* bgr: N frames uint8 [H][W][3] (row stride `row_stride` bytes, frame stride
+ * `frame_stride` bytes); records: N * opose_body_record_bytes(). Returns the worst
+ * per-frame status (each record carries its own). */
+int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W,
+                     int64_t row_stride, int64_t frame_stride, const opose_params* p,
+                     void* records, int flags);
+
+/* Post-network body path on a single scale (what follows src/body.py:50):
+ * maps [N,57,h,w] fp32 (channels 0..37 PAF, 38..56 heat), padded net input (h*8, w*8),
+ * pad_down / pad_right as util.padRightDownCorner, frame H x W. */
+int opose_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int pad_down,
+                    int pad_right, int H, int W, const opose_params* p, void* records, int flags);
+
+/* Hand on N square crops uint8 [S][S][3]: peaks [N][21][3] (x, y, score), found [N][21]
+ * (0 = part missing, the reference's [0,0,0] row). */
+int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int S, int64_t row_stride,
+                     int64_t frame_stride, const opose_params* p, double* peaks,
+                     int32_t* found, int flags);
+
+/* Post-network hand path: maps[s] = [N,22,hl[s],wl[s]] per scale s (pads per scale). */
+int opose_hand_post(opose_t* h, const float* const* maps, const int* hl, const int* wl,
+                    const int* pad_down, const int* pad_right, int n_scales, int N, int S,
+                    const opose_params* p, double* peaks, int32_t* found, int flags);
+
+/* ---- measurement ---------------------------------------------------------------------- */
+/* When enabled, every kernel launch is bracketed by HIP events on the handle's stream and
+ * accumulated per kernel class.  opose_profile_read writes one JSON object. */
+int opose_profile_enable(opose_t* h, int enable);
+int opose_profile_reset(opose_t* h);
+int opose_profile_read(opose_t* h, char* buf, size_t len);
+
+/* ---- test hooks (parity tests call single stages; host pointers, synchronous) ----- */
+/* one stride-1 conv: x [N,Cin,H,W], w [Cout,Cin,ks,ks], b [Cout] -> out [N,Cout,H,W];
+ * mt/pt/splits <= 0 select the production tile heuristic */
+int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b, int N, int Cin, int H, int W,
+                     int Cout, int ks, int pad, int relu, int mt, int pt, int splits, float* out);
+/* src/body.py:38-41 for one frame and one scale: out [3,Hp,Wp]; HpWp receives (Hp, Wp)
+ * (out may be NULL to query the size) */
+int opose_debug_preprocess(opose_t* h, const uint8_t* bgr, int H, int W, double scale, int pad_value,
+                           float* out, int* HpWp);
+/* src/body.py:54-57,67 for one frame: maps [57,hl,wl] -> heat_avg [18,H,W] float64 and
+ * (optional) the x8-upsampled, cropped PAF maps [38,Hs,Ws] float32 */
+int opose_debug_heat(opose_t* h, const float* maps, int hl, int wl, int pad_down, int pad_right, int H, int W,
+                     double* heat_avg, float* paf_mid);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OPOSE_H */

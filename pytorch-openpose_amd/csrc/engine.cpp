@@ -1,0 +1,948 @@
+// engine.cpp — libopose host runtime: weights, network plans, workspace, C ABI.
+//
+// Mirrors hitmaxiang/pytorch-openpose:
+//  * topology + state_dict order      src/model.py:25-104 (body), :136-195 (hand)
+//  * Body.__call__ orchestration      src/body.py:24-212
+//  * Hand.__call__ orchestration      src/hand.py:25-75
+// The network runs as ~60 launches of the implicit-GEMM conv kernel (conv.hip); the two
+// CPM branches of a stage share one launch (combined M for their common first conv,
+// two GEMM groups for the rest); stage concatenation is implicit (channel-slice writes).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/opose.h"
+#include "common.h"
+#include "kernels.h"
+
+using namespace opose;
+
+namespace {
+
+struct Spec {
+    std::string name;
+    int cin, cout, ks, pad;
+};
+
+// ---------------------------------------------------------------- topology (src/model.py)
+std::vector<Spec> vgg_body() {
+    return {{"conv1_1", 3, 64, 3, 1},     {"conv1_2", 64, 64, 3, 1},     {"conv2_1", 64, 128, 3, 1},
+            {"conv2_2", 128, 128, 3, 1},  {"conv3_1", 128, 256, 3, 1},   {"conv3_2", 256, 256, 3, 1},
+            {"conv3_3", 256, 256, 3, 1},  {"conv3_4", 256, 256, 3, 1},   {"conv4_1", 256, 512, 3, 1},
+            {"conv4_2", 512, 512, 3, 1},  {"conv4_3_CPM", 512, 256, 3, 1}, {"conv4_4_CPM", 256, 128, 3, 1}};
+}
+std::vector<Spec> vgg_hand() {
+    return {{"conv1_1", 3, 64, 3, 1},    {"conv1_2", 64, 64, 3, 1},    {"conv2_1", 64, 128, 3, 1},
+            {"conv2_2", 128, 128, 3, 1}, {"conv3_1", 128, 256, 3, 1},  {"conv3_2", 256, 256, 3, 1},
+            {"conv3_3", 256, 256, 3, 1}, {"conv3_4", 256, 256, 3, 1},  {"conv4_1", 256, 512, 3, 1},
+            {"conv4_2", 512, 512, 3, 1}, {"conv4_3", 512, 512, 3, 1},  {"conv4_4", 512, 512, 3, 1},
+            {"conv5_1", 512, 512, 3, 1}, {"conv5_2", 512, 512, 3, 1},  {"conv5_3_CPM", 512, 128, 3, 1}};
+}
+std::vector<Spec> body_branch(int stage, int br) {
+    const int out = br == 1 ? 38 : 19;
+    const std::string L = "_L" + std::to_string(br);
+    if (stage == 1)
+        return {{"conv5_1_CPM" + L, 128, 128, 3, 1}, {"conv5_2_CPM" + L, 128, 128, 3, 1},
+                {"conv5_3_CPM" + L, 128, 128, 3, 1}, {"conv5_4_CPM" + L, 128, 512, 1, 0},
+                {"conv5_5_CPM" + L, 512, out, 1, 0}};
+    const std::string sfx = "_stage" + std::to_string(stage) + L;
+    std::vector<Spec> v = {{"Mconv1" + sfx, 185, 128, 7, 3}};
+    for (int i = 2; i <= 5; ++i) v.push_back({"Mconv" + std::to_string(i) + sfx, 128, 128, 7, 3});
+    v.push_back({"Mconv6" + sfx, 128, 128, 1, 0});
+    v.push_back({"Mconv7" + sfx, 128, out, 1, 0});
+    return v;
+}
+std::vector<Spec> hand_stage(int stage) {
+    if (stage == 1) return {{"conv6_1_CPM", 128, 512, 1, 0}, {"conv6_2_CPM", 512, 22, 1, 0}};
+    const std::string sfx = "_stage" + std::to_string(stage);
+    std::vector<Spec> v = {{"Mconv1" + sfx, 150, 128, 7, 3}};
+    for (int i = 2; i <= 5; ++i) v.push_back({"Mconv" + std::to_string(i) + sfx, 128, 128, 7, 3});
+    v.push_back({"Mconv6" + sfx, 128, 128, 1, 0});
+    v.push_back({"Mconv7" + sfx, 128, 22, 1, 0});
+    return v;
+}
+std::vector<Spec> state_dict_order(int net) {
+    std::vector<Spec> all;
+    if (net == OPOSE_NET_BODY) {
+        all = vgg_body();
+        for (int br = 1; br <= 2; ++br)
+            for (int s = 1; s <= 6; ++s) {
+                auto b = body_branch(s, br);
+                all.insert(all.end(), b.begin(), b.end());
+            }
+    } else {
+        all = vgg_hand();
+        for (int s = 1; s <= 6; ++s) {
+            auto b = hand_stage(s);
+            all.insert(all.end(), b.begin(), b.end());
+        }
+    }
+    return all;
+}
+
+int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+// ---------------------------------------------------------------- device memory helpers
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    template <class T>
+    T* ensure(size_t n, hipStream_t st) {
+        size_t b = n * sizeof(T);
+        if (b > bytes) {
+            if (p) {
+                OPOSE_HIP_CHECK(hipStreamSynchronize(st));
+                OPOSE_HIP_CHECK(hipFree(p));
+                p = nullptr;
+            }
+            size_t nb = std::max(b, bytes + bytes / 4);
+            OPOSE_HIP_CHECK(hipMalloc(&p, nb));
+            bytes = nb;
+        }
+        return static_cast<T*>(p);
+    }
+};
+
+// A GEMM-ready conv: one or two (combined) reference layers.
+struct DevConv {
+    std::string name;
+    int cin = 0, cout = 0, ks = 0, pad = 0, K = 0, Kpad = 0, Mpad = 0;
+    float* wt = nullptr;
+    float* bias = nullptr;
+    int* ktab = nullptr;
+    ~DevConv() {
+        if (wt) (void)hipFree(wt);
+        if (bias) (void)hipFree(bias);
+        if (ktab) (void)hipFree(ktab);
+    }
+};
+
+struct ProfEntry {
+    std::string cls;
+    double flops;
+    double bytes;
+    hipEvent_t e0, e1;
+};
+
+struct ProfAgg {
+    long count = 0;
+    double ms = 0, flops = 0, bytes = 0;
+};
+
+}  // namespace
+
+struct opose_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int ppp = 128, maxp = 96;
+    // weights
+    std::map<std::string, std::unique_ptr<DevConv>> convs[2];
+    bool loaded[2] = {false, false};
+    // workspace
+    DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[kMaxScales], avg, cnt, list, peak_pos, part_cnt,
+        score, conn, conn_cnt, records, maps_in;
+    // profiling
+    bool prof = false;
+    std::vector<ProfEntry> pending;
+    std::map<std::string, ProfAgg> agg;
+    std::vector<hipEvent_t> event_pool;
+
+    hipEvent_t get_event() {
+        if (!event_pool.empty()) {
+            hipEvent_t e = event_pool.back();
+            event_pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        OPOSE_HIP_CHECK(hipEventCreate(&e));
+        return e;
+    }
+    void prof_begin(ProfEntry& pe, const char* cls, double flops, double bytes) {
+        if (!prof) return;
+        pe.cls = cls;
+        pe.flops = flops;
+        pe.bytes = bytes;
+        pe.e0 = get_event();
+        pe.e1 = get_event();
+        OPOSE_HIP_CHECK(hipEventRecord(pe.e0, stream));
+    }
+    void prof_end(ProfEntry& pe) {
+        if (!prof) return;
+        OPOSE_HIP_CHECK(hipEventRecord(pe.e1, stream));
+        pending.push_back(pe);
+    }
+    void prof_drain() {
+        for (auto& pe : pending) {
+            OPOSE_HIP_CHECK(hipEventSynchronize(pe.e1));
+            float ms = 0;
+            OPOSE_HIP_CHECK(hipEventElapsedTime(&ms, pe.e0, pe.e1));
+            auto& a = agg[pe.cls];
+            a.count++;
+            a.ms += ms;
+            a.flops += pe.flops;
+            a.bytes += pe.bytes;
+            event_pool.push_back(pe.e0);
+            event_pool.push_back(pe.e1);
+        }
+        pending.clear();
+    }
+    ~opose_ctx() {
+        for (auto e : event_pool) (void)hipEventDestroy(e);
+        if (own_stream) (void)hipStreamDestroy(own_stream);
+    }
+};
+
+namespace {
+
+struct Act {  // a channel slice of an NCHW activation buffer
+    float* p;
+    int cstride, coff;
+};
+
+// --------------------------------------------------------------- conv launch planning
+struct TileChoice {
+    int mt, pt, splits, cps;
+};
+
+TileChoice choose_tile(int Mpad, int npix, int ngroups, int nchunks) {
+    // Cost model in units of one 32-deep k-chunk of a 64x64 tile on one CU (~0.42 us at
+    // the fp32 MFMA rate).  A CU running k >= 2 co-resident workgroups finishes them in
+    // k * work; a lone workgroup (one wave per SIMD) only reaches ~60 % of the MFMA rate.
+    static const int cfg[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+    static const double ovh[4] = {1.0, 1.10, 1.10, 1.30};  // load/issue overhead per MFMA
+    TileChoice best{64, 64, 1, nchunks};
+    double best_cost = 1e300;
+    for (int c = 0; c < 4; ++c) {
+        const int mt = cfg[c][0], pt = cfg[c][1];
+        if (Mpad % mt) continue;
+        const long tiles = (long)(Mpad / mt) * ((npix + pt - 1) / pt) * ngroups;
+        for (int s = 1; s <= 64; s *= 2) {
+            const int cps = (nchunks + s - 1) / s;
+            if (s > 1 && cps < 4) break;
+            const long wgs = tiles * s;
+            const double per_cu = std::max<double>((wgs + 255) / 256, 1.6);
+            double cost = per_cu * cps * (mt / 64.0) * (pt / 64.0) * ovh[c];
+            if (s > 1) {  // slab write + ordered re-read + one extra launch (~2 us)
+                const double bytes = 8.0 * s * Mpad * (double)npix * ngroups;
+                cost += bytes / 5e12 / 0.42e-6 + 5.0;
+            }
+            if (cost < best_cost * 0.97) {
+                best_cost = cost;
+                best = {mt, pt, s, cps};
+            }
+        }
+    }
+    return best;
+}
+
+}  // namespace
+
+// ======================================================================== engine
+namespace opose {
+
+static DevConv* find_conv(opose_ctx* h, int net, const std::string& name) {
+    auto it = h->convs[net].find(name);
+    if (it == h->convs[net].end()) throw std::runtime_error("missing layer " + name);
+    return it->second.get();
+}
+
+static void upload_conv(opose_ctx* h, int net, const std::string& key, const std::vector<const Spec*>& parts,
+                        const std::vector<const float*>& w, const std::vector<const float*>& b) {
+    auto dc = std::make_unique<DevConv>();
+    const Spec& s0 = *parts[0];
+    dc->name = key;
+    dc->cin = s0.cin;
+    dc->ks = s0.ks;
+    dc->pad = s0.pad;
+    dc->K = s0.cin * s0.ks * s0.ks;
+    dc->Kpad = round_up(dc->K, 32);
+    int cout = 0;
+    for (auto* p : parts) cout += p->cout;
+    dc->cout = cout;
+    dc->Mpad = cout <= 64 ? 64 : round_up(cout, 128);
+    std::vector<float> wt((size_t)dc->Kpad * dc->Mpad, 0.f), bias(cout, 0.f);
+    int m0 = 0;
+    for (size_t i = 0; i < parts.size(); ++i) {
+        for (int m = 0; m < parts[i]->cout; ++m) {
+            for (int k = 0; k < dc->K; ++k) wt[(size_t)k * dc->Mpad + m0 + m] = w[i][(size_t)m * dc->K + k];
+            bias[m0 + m] = b[i][m];
+        }
+        m0 += parts[i]->cout;
+    }
+    std::vector<int> ktab(dc->Kpad, -1);
+    for (int k = 0; k < dc->K; ++k) {
+        int c = k / (dc->ks * dc->ks), r = k % (dc->ks * dc->ks);
+        ktab[k] = (c << 8) | ((r / dc->ks) << 4) | (r % dc->ks);
+    }
+    OPOSE_HIP_CHECK(hipMalloc(&dc->wt, wt.size() * 4));
+    OPOSE_HIP_CHECK(hipMalloc(&dc->bias, bias.size() * 4));
+    OPOSE_HIP_CHECK(hipMalloc(&dc->ktab, ktab.size() * 4));
+    OPOSE_HIP_CHECK(hipMemcpy(dc->wt, wt.data(), wt.size() * 4, hipMemcpyHostToDevice));
+    OPOSE_HIP_CHECK(hipMemcpy(dc->bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
+    OPOSE_HIP_CHECK(hipMemcpy(dc->ktab, ktab.data(), ktab.size() * 4, hipMemcpyHostToDevice));
+    h->convs[net][key] = std::move(dc);
+}
+
+static const char* conv_class(int ks) { return ks == 7 ? "conv7x7" : (ks == 3 ? "conv3x3" : "conv1x1"); }
+
+// run one (possibly 2-group) conv: out = act(conv(in))
+static void run_conv(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W, Act in0, Act out0, Act in1,
+                     Act out1, bool relu0, bool relu1, Act dup = {nullptr, 0, 0}) {
+    ConvArgs a{};
+    const int ng = c1 ? 2 : 1;
+    a.N = N;
+    a.H = H;
+    a.W = W;
+    a.Cin = c0->cin;
+    a.ks = c0->ks;
+    a.pad = c0->pad;
+    a.K = c0->K;
+    a.Kpad = c0->Kpad;
+    a.Mpad = c0->Mpad;
+    a.npix = N * H * W;
+    DevConv* cs[2] = {c0, c1};
+    Act ins[2] = {in0, in1}, outs[2] = {out0, out1};
+    bool relus[2] = {relu0, relu1};
+    for (int g = 0; g < ng; ++g) {
+        ConvGroup& G = a.g[g];
+        G.in = ins[g].p;
+        G.in_cstride = ins[g].cstride;
+        G.in_coff = ins[g].coff;
+        G.wt = cs[g]->wt;
+        G.bias = cs[g]->bias;
+        G.out = outs[g].p;
+        G.out_cstride = outs[g].cstride;
+        G.out_coff = outs[g].coff;
+        G.out2 = nullptr;
+        G.cout = cs[g]->cout;
+        G.relu = relus[g] ? 1 : 0;
+    }
+    if (dup.p) {
+        a.g[0].out2 = dup.p;
+        a.g[0].out2_cstride = dup.cstride;
+        a.g[0].out2_coff = dup.coff;
+    }
+    if (ng == 1) a.g[1] = a.g[0];
+    const TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.Kpad / 32);
+    a.splits = t.splits;
+    a.chunks_per_split = t.cps;
+    if (t.splits > 1) a.partial = h->partial.ensure<float>((size_t)ng * t.splits * a.Mpad * a.npix, h->stream);
+    double flops = 0;
+    for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)a.K * a.npix;
+    ProfEntry pe;
+    h->prof_begin(pe, conv_class(c0->ks), flops, 0);
+    launch_conv(a, ng, c0->ktab, t.mt, t.pt, h->stream);
+    h->prof_end(pe);
+}
+
+static void run_pool(opose_ctx* h, const float* in, float* out, int NC, int H, int W) {
+    ProfEntry pe;
+    h->prof_begin(pe, "maxpool", 0, (double)NC * H * W * 4 * 1.25);
+    launch_maxpool(in, out, NC, H, W, h->stream);
+    h->prof_end(pe);
+}
+
+// VGG trunk: x [N,3,H,W] -> final trunk conv written via `last` (+ optional duplicate)
+static void run_trunk(opose_ctx* h, int net, const float* x, int N, int H, int W, Act last, Act dup) {
+    const std::vector<Spec> vgg = net == OPOSE_NET_BODY ? vgg_body() : vgg_hand();
+    size_t act = (size_t)N * 64 * H * W;
+    float* A = h->bufA.ensure<float>(act, h->stream);
+    float* B = h->bufB.ensure<float>(act, h->stream);
+    const float* cur = x;
+    int cc = 3, hh = H, ww = W;
+    for (size_t i = 0; i < vgg.size(); ++i) {
+        const Spec& s = vgg[i];
+        DevConv* c = find_conv(h, net, s.name);
+        const bool final_layer = i + 1 == vgg.size();
+        float* dst = (cur == A) ? B : A;
+        Act out = final_layer ? last : Act{dst, s.cout, 0};
+        run_conv(h, c, nullptr, N, hh, ww, Act{const_cast<float*>(cur), cc, 0}, out, Act{}, Act{}, true, false,
+                 final_layer ? dup : Act{nullptr, 0, 0});
+        cur = dst;
+        cc = s.cout;
+        // pools follow conv1_2, conv2_2, conv3_4 (src/model.py:37,40,45 / :147,150,155)
+        if (s.name == "conv1_2" || s.name == "conv2_2" || s.name == "conv3_4") {
+            float* pd = (cur == A) ? B : A;
+            run_pool(h, cur, pd, N * cc, hh, ww);
+            hh /= 2;
+            ww /= 2;
+            cur = pd;
+        }
+    }
+}
+
+// bodypose_model.forward (src/model.py:106-133). Output: S-buffer with paf [0,38), heat [38,57)
+static float* body_net(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
+    if (!h->loaded[OPOSE_NET_BODY]) throw std::runtime_error("body weights not loaded");
+    const int hl = Hp / 8, wl = Wp / 8;
+    const size_t px = (size_t)N * hl * wl;
+    float* S[2] = {h->S0.ensure<float>(px * 185, h->stream), h->S1.ensure<float>(px * 185, h->stream)};
+    float* T[2] = {h->T0.ensure<float>(px * 256, h->stream), h->T1.ensure<float>(px * 256, h->stream)};
+    float* U = h->U.ensure<float>(px * 1024, h->stream);
+    const int net = OPOSE_NET_BODY;
+    run_trunk(h, net, x, N, Hp, Wp, Act{S[0], 185, 57}, Act{S[1], 185, 57});
+    // stage 1 (src/model.py:52-62): input = trunk slice of S0
+    run_conv(h, find_conv(h, net, "conv5_1_CPM_L1+L2"), nullptr, N, hl, wl, Act{S[0], 185, 57}, Act{T[0], 256, 0},
+             Act{}, Act{}, true, false);
+    run_conv(h, find_conv(h, net, "conv5_2_CPM_L1"), find_conv(h, net, "conv5_2_CPM_L2"), N, hl, wl,
+             Act{T[0], 256, 0}, Act{T[1], 256, 0}, Act{T[0], 256, 128}, Act{T[1], 256, 128}, true, true);
+    run_conv(h, find_conv(h, net, "conv5_3_CPM_L1"), find_conv(h, net, "conv5_3_CPM_L2"), N, hl, wl,
+             Act{T[1], 256, 0}, Act{T[0], 256, 0}, Act{T[1], 256, 128}, Act{T[0], 256, 128}, true, true);
+    run_conv(h, find_conv(h, net, "conv5_4_CPM_L1"), find_conv(h, net, "conv5_4_CPM_L2"), N, hl, wl,
+             Act{T[0], 256, 0}, Act{U, 1024, 0}, Act{T[0], 256, 128}, Act{U, 1024, 512}, true, true);
+    run_conv(h, find_conv(h, net, "conv5_5_CPM_L1"), find_conv(h, net, "conv5_5_CPM_L2"), N, hl, wl,
+             Act{U, 1024, 0}, Act{S[1], 185, 0}, Act{U, 1024, 512}, Act{S[1], 185, 38}, false, false);
+    int cur = 1;
+    for (int st = 2; st <= 6; ++st) {
+        const std::string s = "_stage" + std::to_string(st);
+        float* in = S[cur];
+        float* out = S[cur ^ 1];
+        run_conv(h, find_conv(h, net, "Mconv1" + s + "_L1+L2"), nullptr, N, hl, wl, Act{in, 185, 0},
+                 Act{T[0], 256, 0}, Act{}, Act{}, true, false);
+        int t = 0;
+        for (int i = 2; i <= 6; ++i) {
+            const std::string nm = "Mconv" + std::to_string(i) + s;
+            run_conv(h, find_conv(h, net, nm + "_L1"), find_conv(h, net, nm + "_L2"), N, hl, wl, Act{T[t], 256, 0},
+                     Act{T[t ^ 1], 256, 0}, Act{T[t], 256, 128}, Act{T[t ^ 1], 256, 128}, true, true);
+            t ^= 1;
+        }
+        // Mconv7: no ReLU, except Mconv7_stage6_L2 (no_relu list quirk, src/model.py:30-33)
+        run_conv(h, find_conv(h, net, "Mconv7" + s + "_L1"), find_conv(h, net, "Mconv7" + s + "_L2"), N, hl, wl,
+                 Act{T[t], 256, 0}, Act{out, 185, 0}, Act{T[t], 256, 128}, Act{out, 185, 38}, false, st == 6);
+        cur ^= 1;
+    }
+    return S[cur];
+}
+
+// handpose_model.forward (src/model.py:197-214). Output: S-buffer with heat [0,22)
+static float* hand_net(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
+    if (!h->loaded[OPOSE_NET_HAND]) throw std::runtime_error("hand weights not loaded");
+    const int hl = Hp / 8, wl = Wp / 8;
+    const size_t px = (size_t)N * hl * wl;
+    float* S[2] = {h->S0.ensure<float>(px * 150, h->stream), h->S1.ensure<float>(px * 150, h->stream)};
+    float* T[2] = {h->T0.ensure<float>(px * 128, h->stream), h->T1.ensure<float>(px * 128, h->stream)};
+    float* U = h->U.ensure<float>(px * 512, h->stream);
+    const int net = OPOSE_NET_HAND;
+    run_trunk(h, net, x, N, Hp, Wp, Act{S[0], 150, 22}, Act{S[1], 150, 22});
+    run_conv(h, find_conv(h, net, "conv6_1_CPM"), nullptr, N, hl, wl, Act{S[0], 150, 22}, Act{U, 512, 0}, Act{},
+             Act{}, true, false);
+    run_conv(h, find_conv(h, net, "conv6_2_CPM"), nullptr, N, hl, wl, Act{U, 512, 0}, Act{S[1], 150, 0}, Act{},
+             Act{}, false, false);
+    int cur = 1;
+    for (int st = 2; st <= 6; ++st) {
+        const std::string s = "_stage" + std::to_string(st);
+        float* in = S[cur];
+        float* out = S[cur ^ 1];
+        run_conv(h, find_conv(h, net, "Mconv1" + s), nullptr, N, hl, wl, Act{in, 150, 0}, Act{T[0], 128, 0}, Act{},
+                 Act{}, true, false);
+        int t = 0;
+        for (int i = 2; i <= 6; ++i) {
+            run_conv(h, find_conv(h, net, "Mconv" + std::to_string(i) + s), nullptr, N, hl, wl, Act{T[t], 128, 0},
+                     Act{T[t ^ 1], 128, 0}, Act{}, Act{}, true, false);
+            t ^= 1;
+        }
+        run_conv(h, find_conv(h, net, "Mconv7" + s), nullptr, N, hl, wl, Act{T[t], 128, 0}, Act{out, 150, 0}, Act{},
+                 Act{}, false, false);
+        cur ^= 1;
+    }
+    return S[cur];
+}
+
+// ---------------------------------------------------------------- geometry (src/body.py:32-41)
+struct ScaleGeom {
+    double mult;      // scale * boxsize / H
+    int Hs, Ws;       // cv2.resize output (cvRound(H * mult))
+    int Hp, Wp;       // padded to stride
+    int hl, wl;       // network output
+    double up_sy, up_sx;  // final resize (Hs,Ws) -> (H,W) source steps
+};
+
+static int cv_round(double v) { return (int)std::nearbyint(v); }
+
+static ScaleGeom geom(double s, const opose_params& p, int H, int W) {
+    ScaleGeom g;
+    g.mult = s * p.boxsize / H;
+    g.Hs = cv_round(H * g.mult);
+    g.Ws = cv_round(W * g.mult);
+    if (g.Hs <= 0 || g.Ws <= 0) throw std::invalid_argument("scale produces an empty image");
+    g.Hp = round_up(g.Hs, p.stride);
+    g.Wp = round_up(g.Ws, p.stride);
+    g.hl = g.Hp / 8;
+    g.wl = g.Wp / 8;
+    g.up_sy = 1.0 / ((double)H / g.Hs);
+    g.up_sx = 1.0 / ((double)W / g.Ws);
+    return g;
+}
+
+// post-network body path from per-scale x8 maps (mids) to records
+static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vector<ScaleGeom>& gs,
+                             const opose_params& p, uint8_t* rec_dev) {
+    const RecordLayout L = make_record_layout(h->ppp, h->maxp);
+    const int cap = h->ppp;
+    const int ns = (int)gs.size();
+    double* avg = h->avg.ensure<double>((size_t)N * 18 * H * W, h->stream);
+    ProfEntry pe;
+    for (int s = 0; s < ns; ++s) {
+        h->prof_begin(pe, "heat_full", 0, (double)N * 18 * H * W * 8 * (s ? 2 : 1));
+        launch_heat_full(h->mids[s].ensure<float>(0, h->stream), 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W,
+                         gs[s].up_sy, gs[s].up_sx, ns, s > 0, avg, h->stream);
+        h->prof_end(pe);
+    }
+    int* cnt = h->cnt.ensure<int>((size_t)N * 18, h->stream);
+    int* list = h->list.ensure<int>((size_t)N * 18 * cap, h->stream);
+    int* pos = h->peak_pos.ensure<int>((size_t)N * 18 * cap, h->stream);
+    int* pcnt = h->part_cnt.ensure<int>((size_t)N * 18, h->stream);
+    double* score = h->score.ensure<double>((size_t)N * 19 * cap * cap, h->stream);
+    Conn* conn = h->conn.ensure<Conn>((size_t)N * 19 * cap, h->stream);
+    int* ccnt = h->conn_cnt.ensure<int>((size_t)N * 19, h->stream);
+    OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * N * 18, h->stream));
+    h->prof_begin(pe, "gauss_nms", 0, (double)N * 18 * H * W * 8);
+    launch_gauss_nms(avg, N * 18, H, W, p.thre1, cap, cnt, list, h->stream);
+    h->prof_end(pe);
+    h->prof_begin(pe, "peaks_finalize", 0, 0);
+    launch_peaks_finalize(cnt, list, avg, N, H, W, L, rec_dev, pos, pcnt, h->stream);
+    h->prof_end(pe);
+    PafScales S{};
+    for (int s = 0; s < ns; ++s) {
+        S.mid[s] = h->mids[s].ensure<float>(0, h->stream);
+        S.hs[s] = gs[s].Hs;
+        S.ws[s] = gs[s].Ws;
+        S.sy[s] = gs[s].up_sy;
+        S.sx[s] = gs[s].up_sx;
+    }
+    S.n = ns;
+    S.cm = 56;
+    S.H = H;
+    S.W = W;
+    h->prof_begin(pe, "paf_score", 0, 0);
+    launch_paf_score(S, pos, pcnt, N, cap, p.thre2, score, h->stream);
+    h->prof_end(pe);
+    h->prof_begin(pe, "limb_greedy", 0, 0);
+    launch_limb_greedy(score, pcnt, N, cap, conn, ccnt, h->stream);
+    h->prof_end(pe);
+    h->prof_begin(pe, "assemble", 0, 0);
+    launch_assemble(conn, ccnt, pcnt, N, L, rec_dev, h->stream);
+    h->prof_end(pe);
+}
+
+static void upsample_to_mid(opose_ctx* h, int s, const float* maps, int cstride, int N, const ScaleGeom& g, int C) {
+    float* mid = h->mids[s].ensure<float>((size_t)N * C * g.Hs * g.Ws, h->stream);
+    ProfEntry pe;
+    h->prof_begin(pe, "upsample8", 0, (double)N * C * g.Hs * g.Ws * 4);
+    launch_upsample8(maps, cstride, 0, C, N, g.hl, g.wl, g.Hs, g.Ws, mid, h->stream);
+    h->prof_end(pe);
+}
+
+static int worst_status(const uint8_t* rec, int N, size_t bytes) {
+    int w = 0;
+    for (int n = 0; n < N; ++n) {
+        int s = reinterpret_cast<const int32_t*>(rec + (size_t)n * bytes)[0];
+        if (s < w) w = s;
+    }
+    return w;
+}
+
+}  // namespace opose
+
+// ======================================================================== C ABI
+#define OPOSE_TRY(h, ...)                      \
+    try {                                      \
+        __VA_ARGS__;                           \
+    } catch (const std::invalid_argument& e) { \
+        if (h) (h)->err = e.what();            \
+        return OPOSE_E_SHAPE;                  \
+    } catch (const opose::HipError& e) {       \
+        if (h) (h)->err = e.what();            \
+        return OPOSE_E_HIP;                    \
+    } catch (const std::exception& e) {        \
+        if (h) (h)->err = e.what();            \
+        return OPOSE_E_WEIGHTS;                \
+    }
+
+extern "C" {
+
+void opose_default_params(int net, opose_params* p) {
+    std::memset(p, 0, sizeof(*p));
+    if (net == OPOSE_NET_HAND) {
+        p->n_scales = 4;
+        p->scales[0] = 0.5;
+        p->scales[1] = 1.0;
+        p->scales[2] = 1.5;
+        p->scales[3] = 2.0;
+    } else {
+        p->n_scales = 1;
+        p->scales[0] = 0.5;
+    }
+    p->boxsize = 368;
+    p->stride = 8;
+    p->pad_value = 128;
+    p->thre1 = 0.1;
+    p->thre2 = 0.05;
+    p->thre_hand = 0.03;
+}
+
+int opose_create(int device, opose_t** out) {
+    if (!out) return OPOSE_E_ARG;
+    *out = nullptr;
+    auto* h = new opose_ctx();
+    h->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return OPOSE_E_HIP;
+    }
+    h->stream = h->own_stream;
+    *out = h;
+    return OPOSE_OK;
+}
+
+void opose_destroy(opose_t* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    delete h;
+}
+
+const char* opose_last_error(const opose_t* h) { return h ? h->err.c_str() : "null handle"; }
+
+int opose_set_stream(opose_t* h, void* s) {
+    if (!h) return OPOSE_E_ARG;
+    h->stream = s ? static_cast<hipStream_t>(s) : h->own_stream;
+    return OPOSE_OK;
+}
+
+void* opose_get_stream(const opose_t* h) { return h ? h->stream : nullptr; }
+
+int opose_synchronize(opose_t* h) {
+    if (!h) return OPOSE_E_ARG;
+    OPOSE_TRY(h, OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream)));
+    return OPOSE_OK;
+}
+
+int opose_set_capacity(opose_t* h, int ppp, int maxp) {
+    if (!h || ppp < 1 || maxp < 1 || ppp > 1024 || maxp > 256) return OPOSE_E_ARG;
+    h->ppp = ppp;
+    h->maxp = maxp;
+    return OPOSE_OK;
+}
+
+size_t opose_body_record_bytes(const opose_t* h) { return h ? make_record_layout(h->ppp, h->maxp).bytes : 0; }
+
+int opose_load_weights(opose_t* h, int net, const float* const* tensors, const int64_t* shapes, int n) {
+    if (!h || !tensors || !shapes || (net != OPOSE_NET_BODY && net != OPOSE_NET_HAND)) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const std::vector<Spec> order = state_dict_order(net);
+        if ((size_t)n != 2 * order.size()) {
+            h->err = "expected " + std::to_string(2 * order.size()) + " tensors, got " + std::to_string(n);
+            return OPOSE_E_WEIGHTS;
+        }
+        std::map<std::string, std::pair<const float*, const float*>> byname;
+        for (size_t i = 0; i < order.size(); ++i) {
+            const Spec& s = order[i];
+            const int64_t* ws = shapes + 8 * i;
+            const int64_t* bs = shapes + 8 * i + 4;
+            if (ws[0] != s.cout || ws[1] != s.cin || ws[2] != s.ks || ws[3] != s.ks || bs[0] != s.cout) {
+                h->err = "shape mismatch for " + s.name;
+                return OPOSE_E_WEIGHTS;
+            }
+            byname[s.name] = {tensors[2 * i], tensors[2 * i + 1]};
+        }
+        h->convs[net].clear();
+        for (const Spec& s : order)
+            upload_conv(h, net, s.name, {&s}, {byname[s.name].first}, {byname[s.name].second});
+        if (net == OPOSE_NET_BODY) {
+            // branch-pair layers sharing an input become one GEMM with M = 256
+            std::vector<std::string> shared = {"conv5_1_CPM"};
+            for (int st = 2; st <= 6; ++st) shared.push_back("Mconv1_stage" + std::to_string(st));
+            for (const auto& base : shared) {
+                const std::string l1 = base + "_L1", l2 = base + "_L2";
+                const Spec *s1 = nullptr, *s2 = nullptr;
+                for (const Spec& s : order) {
+                    if (s.name == l1) s1 = &s;
+                    if (s.name == l2) s2 = &s;
+                }
+                upload_conv(h, net, base + "_L1+L2", {s1, s2}, {byname[l1].first, byname[l2].first},
+                            {byname[l1].second, byname[l2].second});
+            }
+        }
+        h->loaded[net] = true;
+    });
+    return OPOSE_OK;
+}
+
+static int net_forward(opose_t* h, int net, const float* x, int N, int Hp, int Wp, float* o1, float* o2, int flags) {
+    if (!h || !x || N <= 0 || Hp < 8 || Wp < 8 || Hp % 8 || Wp % 8) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const size_t in_n = (size_t)N * 3 * Hp * Wp;
+        const float* xd = x;
+        if (!(flags & OPOSE_IN_DEVICE)) {
+            float* buf = h->x.ensure<float>(in_n, h->stream);
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, x, in_n * 4, hipMemcpyHostToDevice, h->stream));
+            xd = buf;
+        }
+        const int hl = Hp / 8, wl = Wp / 8;
+        const size_t plane = (size_t)hl * wl;
+        const hipMemcpyKind kind = (flags & OPOSE_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        if (net == OPOSE_NET_BODY) {
+            float* S = body_net(h, xd, N, Hp, Wp);
+            // S: [N][185][hl][wl]; paf = ch 0..37, heat = 38..56
+            OPOSE_HIP_CHECK(hipMemcpy2DAsync(o1, 38 * plane * 4, S, 185 * plane * 4, 38 * plane * 4, N, kind, h->stream));
+            OPOSE_HIP_CHECK(hipMemcpy2DAsync(o2, 19 * plane * 4, S + 38 * plane, 185 * plane * 4, 19 * plane * 4, N,
+                                             kind, h->stream));
+        } else {
+            float* S = hand_net(h, xd, N, Hp, Wp);
+            OPOSE_HIP_CHECK(hipMemcpy2DAsync(o1, 22 * plane * 4, S, 150 * plane * 4, 22 * plane * 4, N, kind, h->stream));
+        }
+        if (!(flags & OPOSE_OUT_DEVICE)) OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+        h->prof_drain();
+    });
+    return OPOSE_OK;
+}
+
+int opose_body_forward(opose_t* h, const float* x, int N, int Hp, int Wp, float* paf, float* heat, int flags) {
+    if (!paf || !heat) return OPOSE_E_ARG;
+    return net_forward(h, OPOSE_NET_BODY, x, N, Hp, Wp, paf, heat, flags);
+}
+
+int opose_hand_forward(opose_t* h, const float* x, int N, int Hp, int Wp, float* heat, int flags) {
+    if (!heat) return OPOSE_E_ARG;
+    return net_forward(h, OPOSE_NET_HAND, x, N, Hp, Wp, heat, nullptr, flags);
+}
+
+static int finish_records(opose_t* h, int N, void* records, uint8_t* rec_dev, int flags) {
+    const RecordLayout L = make_record_layout(h->ppp, h->maxp);
+    if (flags & OPOSE_OUT_DEVICE) {
+        if (rec_dev != records)
+            OPOSE_HIP_CHECK(hipMemcpyAsync(records, rec_dev, L.bytes * N, hipMemcpyDeviceToDevice, h->stream));
+        h->prof_drain();
+        return OPOSE_OK;
+    }
+    OPOSE_HIP_CHECK(hipMemcpyAsync(records, rec_dev, L.bytes * N, hipMemcpyDeviceToHost, h->stream));
+    OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+    h->prof_drain();
+    return worst_status(static_cast<const uint8_t*>(records), N, L.bytes);
+}
+
+static opose_params fill_params(const opose_params* p, int net) {
+    opose_params q;
+    if (p) q = *p;
+    else opose_default_params(net, &q);
+    if (q.n_scales < 1 || q.n_scales > OPOSE_MAX_SCALES || q.stride != 8 || q.boxsize <= 0)
+        throw std::invalid_argument("bad opose_params");
+    return q;
+}
+
+int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride, int64_t frame_stride,
+                     const opose_params* pp, void* records, int flags) {
+    if (!h || !bgr || !records || N <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
+    if (row_stride < (int64_t)W * 3 || frame_stride < row_stride * H) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const opose_params p = fill_params(pp, OPOSE_NET_BODY);
+        const RecordLayout L = make_record_layout(h->ppp, h->maxp);
+        const uint8_t* fd = bgr;
+        if (!(flags & OPOSE_IN_DEVICE)) {
+            uint8_t* buf = h->frames.ensure<uint8_t>((size_t)frame_stride * N, h->stream);
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, (size_t)frame_stride * N, hipMemcpyHostToDevice, h->stream));
+            fd = buf;
+        }
+        std::vector<ScaleGeom> gs;
+        for (int s = 0; s < p.n_scales; ++s) gs.push_back(geom(p.scales[s], p, H, W));
+        for (int s = 0; s < p.n_scales; ++s) {
+            const ScaleGeom& g = gs[s];
+            float* x = h->x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
+            ProfEntry pe;
+            h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
+            launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp, g.Wp,
+                              (float)p.pad_value / 256.f - 0.5f, x, h->stream);
+            h->prof_end(pe);
+            float* S = body_net(h, x, N, g.Hp, g.Wp);
+            upsample_to_mid(h, s, S, 185, N, g, 56);
+        }
+        uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)
+                                                  : h->records.ensure<uint8_t>(L.bytes * N, h->stream);
+        body_post_common(h, N, H, W, gs, p, rec);
+        return finish_records(h, N, records, rec, flags);
+    });
+}
+
+int opose_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int pad_down, int pad_right, int H, int W,
+                    const opose_params* pp, void* records, int flags) {
+    if (!h || !maps || !records || N <= 0 || hl <= 0 || wl <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
+    if (pad_down < 0 || pad_right < 0 || pad_down >= 8 * hl || pad_right >= 8 * wl) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        opose_params p = fill_params(pp, OPOSE_NET_BODY);
+        p.n_scales = 1;
+        const RecordLayout L = make_record_layout(h->ppp, h->maxp);
+        const size_t n_in = (size_t)N * 57 * hl * wl;
+        const float* md = maps;
+        if (!(flags & OPOSE_IN_DEVICE)) {
+            float* buf = h->maps_in.ensure<float>(n_in, h->stream);
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, maps, n_in * 4, hipMemcpyHostToDevice, h->stream));
+            md = buf;
+        }
+        ScaleGeom g;
+        g.mult = 0;
+        g.hl = hl;
+        g.wl = wl;
+        g.Hp = 8 * hl;
+        g.Wp = 8 * wl;
+        g.Hs = g.Hp - pad_down;
+        g.Ws = g.Wp - pad_right;
+        g.up_sy = 1.0 / ((double)H / g.Hs);
+        g.up_sx = 1.0 / ((double)W / g.Ws);
+        upsample_to_mid(h, 0, md, 57, N, g, 56);
+        uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)
+                                                  : h->records.ensure<uint8_t>(L.bytes * N, h->stream);
+        body_post_common(h, N, H, W, {g}, p, rec);
+        return finish_records(h, N, records, rec, flags);
+    });
+}
+
+int opose_hand_infer(opose_t* h, const uint8_t*, int, int, int64_t, int64_t, const opose_params*, double*, int32_t*,
+                     int) {
+    if (h) h->err = "hand path not built yet";
+    return OPOSE_E_SHAPE;
+}
+
+int opose_hand_post(opose_t* h, const float* const*, const int*, const int*, const int*, const int*, int, int, int,
+                    const opose_params*, double*, int32_t*, int) {
+    if (h) h->err = "hand path not built yet";
+    return OPOSE_E_SHAPE;
+}
+
+// ------------------------------------------------------------------ test hooks
+int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b, int N, int Cin, int H, int W,
+                     int Cout, int ks, int pad, int relu, int mt, int pt, int splits, float* out) {
+    if (!h || !x || !w || !b || !out || ks > 15 || pad > 7) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        Spec s{"debug", Cin, Cout, ks, pad};
+        upload_conv(h, 0, "__debug__", {&s}, {w}, {b});
+        DevConv* c = h->convs[0]["__debug__"].get();
+        DevBuf xin, yout;
+        const size_t nx = (size_t)N * Cin * H * W, ny = (size_t)N * Cout * H * W;
+        float* xd = xin.ensure<float>(nx, h->stream);
+        float* yd = yout.ensure<float>(ny, h->stream);
+        OPOSE_HIP_CHECK(hipMemcpyAsync(xd, x, nx * 4, hipMemcpyHostToDevice, h->stream));
+        ConvArgs a{};
+        a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.ks = ks; a.pad = pad;
+        a.K = c->K; a.Kpad = c->Kpad; a.Mpad = c->Mpad; a.npix = N * H * W;
+        ConvGroup& G = a.g[0];
+        G.in = xd; G.in_cstride = Cin; G.in_coff = 0; G.wt = c->wt; G.bias = c->bias;
+        G.out = yd; G.out_cstride = Cout; G.out_coff = 0; G.out2 = nullptr; G.cout = Cout; G.relu = relu;
+        a.g[1] = a.g[0];
+        TileChoice t = choose_tile(a.Mpad, a.npix, 1, a.Kpad / 32);
+        if (mt > 0) { t.mt = mt; t.pt = pt; }
+        if (splits > 0) { t.splits = splits; t.cps = (a.Kpad / 32 + splits - 1) / splits; }
+        if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
+        a.splits = t.splits; a.chunks_per_split = t.cps;
+        if (t.splits > 1) a.partial = h->partial.ensure<float>((size_t)t.splits * a.Mpad * a.npix, h->stream);
+        launch_conv(a, 1, c->ktab, t.mt, t.pt, h->stream);
+        OPOSE_HIP_CHECK(hipMemcpyAsync(out, yd, ny * 4, hipMemcpyDeviceToHost, h->stream));
+        OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+        h->convs[0].erase("__debug__");
+    });
+    return OPOSE_OK;
+}
+
+int opose_debug_preprocess(opose_t* h, const uint8_t* bgr, int H, int W, double scale, int pad_value, float* out,
+                           int* HpWp) {
+    if (!h || !bgr || !HpWp) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        opose_params p;
+        opose_default_params(OPOSE_NET_BODY, &p);
+        const ScaleGeom g = geom(scale, p, H, W);
+        HpWp[0] = g.Hp;
+        HpWp[1] = g.Wp;
+        if (!out) return OPOSE_OK;
+        DevBuf fin, xo;
+        uint8_t* fd = fin.ensure<uint8_t>((size_t)H * W * 3, h->stream);
+        float* xd = xo.ensure<float>((size_t)3 * g.Hp * g.Wp, h->stream);
+        OPOSE_HIP_CHECK(hipMemcpyAsync(fd, bgr, (size_t)H * W * 3, hipMemcpyHostToDevice, h->stream));
+        launch_preprocess(fd, (int64_t)H * W * 3, (int64_t)W * 3, 1, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp,
+                          g.Wp, (float)pad_value / 256.f - 0.5f, xd, h->stream);
+        OPOSE_HIP_CHECK(hipMemcpyAsync(out, xd, (size_t)3 * g.Hp * g.Wp * 4, hipMemcpyDeviceToHost, h->stream));
+        OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+    });
+    return OPOSE_OK;
+}
+
+// maps [57][hl][wl] -> heat_avg [18][H][W] (float64) and PAF x8 map [38][Hs][Ws] (float32)
+int opose_debug_heat(opose_t* h, const float* maps, int hl, int wl, int pad_down, int pad_right, int H, int W,
+                     double* heat_avg, float* paf_mid) {
+    if (!h || !maps || !heat_avg) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        DevBuf min_;
+        float* md = min_.ensure<float>((size_t)57 * hl * wl, h->stream);
+        OPOSE_HIP_CHECK(hipMemcpyAsync(md, maps, (size_t)57 * hl * wl * 4, hipMemcpyHostToDevice, h->stream));
+        ScaleGeom g;
+        g.hl = hl; g.wl = wl; g.Hp = 8 * hl; g.Wp = 8 * wl; g.Hs = g.Hp - pad_down; g.Ws = g.Wp - pad_right;
+        g.up_sy = 1.0 / ((double)H / g.Hs);
+        g.up_sx = 1.0 / ((double)W / g.Ws);
+        upsample_to_mid(h, 0, md, 57, 1, g, 56);
+        double* avg = h->avg.ensure<double>((size_t)18 * H * W, h->stream);
+        launch_heat_full(h->mids[0].ensure<float>(0, h->stream), 56, 38, 18, 1, g.Hs, g.Ws, H, W, g.up_sy, g.up_sx, 1, 0,
+                         avg, h->stream);
+        OPOSE_HIP_CHECK(hipMemcpyAsync(heat_avg, avg, (size_t)18 * H * W * 8, hipMemcpyDeviceToHost, h->stream));
+        if (paf_mid)
+            OPOSE_HIP_CHECK(hipMemcpyAsync(paf_mid, h->mids[0].ensure<float>(0, h->stream),
+                                           (size_t)38 * g.Hs * g.Ws * 4, hipMemcpyDeviceToHost, h->stream));
+        OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+    });
+    return OPOSE_OK;
+}
+
+int opose_profile_enable(opose_t* h, int enable) {
+    if (!h) return OPOSE_E_ARG;
+    h->prof = enable != 0;
+    return OPOSE_OK;
+}
+
+int opose_profile_reset(opose_t* h) {
+    if (!h) return OPOSE_E_ARG;
+    OPOSE_TRY(h, h->prof_drain());
+    h->agg.clear();
+    return OPOSE_OK;
+}
+
+int opose_profile_read(opose_t* h, char* buf, size_t len) {
+    if (!h || !buf || !len) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+        h->prof_drain();
+    });
+    std::string s = "{";
+    bool first = true;
+    for (auto& kv : h->agg) {
+        char tmp[256];
+        std::snprintf(tmp, sizeof tmp, "%s\"%s\":{\"count\":%ld,\"ms\":%.6f,\"flops\":%.6e,\"bytes\":%.6e}",
+                      first ? "" : ",", kv.first.c_str(), kv.second.count, kv.second.ms, kv.second.flops,
+                      kv.second.bytes);
+        s += tmp;
+        first = false;
+    }
+    s += "}";
+    if (s.size() + 1 > len) return OPOSE_E_ARG;
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+    return OPOSE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,46 @@
+// kernels.h — host-side launchers for the libopose kernels.
+#pragma once
+#include "common.h"
+
+namespace opose {
+
+constexpr int kMaxScales = 8;
+
+// x8 maps of every scale for on-demand PAF evaluation (paf_score) and hand heat
+struct PafScales {
+    const float* mid[kMaxScales];  // [N][cm][hs][ws] per scale
+    int hs[kMaxScales], ws[kMaxScales];
+    double sy[kMaxScales], sx[kMaxScales];  // source step of the final resize to H x W
+    int n, cm, H, W;
+};
+
+struct Conn {
+    int i, j;
+    double s;
+};
+
+// conv.hip
+void launch_conv(const ConvArgs& a, int ngroups, const int* ktab, int mt, int pt, hipStream_t st);
+void launch_maxpool(const float* in, float* out, int NC, int H, int W, hipStream_t st);
+
+// imgproc.hip
+void launch_preprocess(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int Hs,
+                       int Ws, double sy, double sx, int Hp, int Wp, float pad_val, float* out, hipStream_t st);
+void launch_upsample8(const float* in, int in_cstride, int in_coff, int C, int N, int hl, int wl, int Hs, int Ws,
+                      float* out, hipStream_t st);
+void launch_heat_full(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
+                      double sx, int nscales, int accumulate, double* avg, hipStream_t st);
+
+// post.hip
+void launch_gauss_nms(const double* avg, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
+                      hipStream_t st);
+void launch_peaks_finalize(const int* cnt, const int* list, const double* avg, int N, int H, int W,
+                           const RecordLayout& L, uint8_t* records, int* peak_pos, int* part_cnt, hipStream_t st);
+void launch_paf_score(const PafScales& S, const int* peak_pos, const int* part_cnt, int N, int cap, double thre2,
+                      double* score, hipStream_t st);
+void launch_limb_greedy(const double* score, const int* part_cnt, int N, int cap, Conn* conn, int* conn_cnt,
+                        hipStream_t st);
+void launch_assemble(const Conn* conn, const int* conn_cnt, const int* part_cnt, int N, const RecordLayout& L,
+                     uint8_t* records, hipStream_t st);
+
+}  // namespace opose

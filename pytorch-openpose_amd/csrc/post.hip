@@ -1,0 +1,413 @@
+// post.hip — the post-network Body path as wavefront-parallel kernels.
+//
+// Reference (hitmaxiang/pytorch-openpose src/body.py), all float64 like the reference:
+//  * :70-94   gaussian_filter(sigma=3) (scipy, mode 'reflect', radius 12) + 4-neighbour
+//             '>=' NMS + '> thre1' + np.nonzero (row-major)      => gauss_nms + peaks_finalize
+//  * :109-141 PAF line integral over 10 linspace samples per (i, j) pair of each limb
+//                                                                => paf_score
+//  * :143-155 stable sort by score (desc) + greedy matching      => limb_greedy
+//  * :157-208 person assembly (found 0/1/2, merge '+1' quirk, IndexError when a third row
+//             matches) + pruning                                  => assemble_people
+// Compiled with -ffp-contract=off: every float64 expression is evaluated in the
+// reference's order with one rounding per operation (bit-exact with NumPy/SciPy).
+#include "common.h"
+#include "cubic.h"
+#include "kernels.h"
+
+namespace opose {
+
+// scipy.ndimage._filters._gaussian_kernel1d(3, 0, 12): centre .. tail (symmetric)
+__constant__ double kGauss[13] = {
+    0x1.105a329f98197p-3, 0x1.01a25f86eb137p-3, 0x1.b42a57d56c0bep-4, 0x1.4a614d1afd337p-4,
+    0x1.bfde9c12bec92p-5, 0x1.0fa58939b528fp-5, 0x1.26defcaeb0202p-6, 0x1.1e6bccad344bap-7,
+    0x1.f1e9915139406p-9, 0x1.8345966f69518p-10, 0x1.0d8a5ad43c165p-11, 0x1.4fbe39149e277p-13,
+    0x1.763a210dfb306p-15};
+
+// src/body.py:97-103
+__constant__ int kLimbA[19] = {1, 1, 2, 3, 5, 6, 1, 8, 9, 1, 11, 12, 1, 0, 14, 0, 15, 2, 5};
+__constant__ int kLimbB[19] = {2, 5, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 0, 14, 16, 15, 17, 16, 17};
+__constant__ int kPafX[19] = {12, 20, 14, 16, 22, 24, 0, 2, 4, 6, 8, 10, 28, 30, 34, 32, 36, 18, 26};
+
+// scipy 'reflect' (d c b a | a b c d | d c b a), periodic with period 2n
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+    const int p = 2 * n;
+    i %= p;
+    if (i < 0) i += p;
+    return i < n ? i : p - 1 - i;
+}
+
+constexpr int GT = 32;        // output tile (GT x GT)
+constexpr int GI = GT + 26;   // input tile incl. 13-pixel halo on each side
+constexpr int GR = GT + 2;    // smoothed rows/cols incl. the NMS ring
+
+// avg: [N*P][H][W] float64; one workgroup per GT x GT tile of one part of one frame.
+__global__ __launch_bounds__(256) void gauss_nms(const double* __restrict__ avg, int P, int H, int W, double thre,
+                                                 int cap, int* __restrict__ cnt, int* __restrict__ list) {
+    __shared__ double s_in[GI][GI];
+    __shared__ double s_v[GR][GI];
+    __shared__ double s_g[GR][GR];
+    const int tid = threadIdx.x;
+    const int x0 = blockIdx.x * GT, y0 = blockIdx.y * GT;
+    const int np = blockIdx.z;
+    const double* m = avg + (size_t)np * H * W;
+
+    for (int e = tid; e < GI * GI; e += 256) {
+        const int r = e / GI, c = e - r * GI;
+        const int gy = reflect_idx(y0 - 13 + r, H), gx = reflect_idx(x0 - 13 + c, W);
+        s_in[r][c] = m[(size_t)gy * W + gx];
+    }
+    __syncthreads();
+    // axis 0 (scipy's first pass): s_v[r][c] = rows y0-1+r, input row index r+12
+    for (int e = tid; e < GR * GI; e += 256) {
+        const int r = e / GI, c = e - r * GI;
+        double acc = s_in[r + 12][c] * kGauss[0];
+        for (int j = 12; j >= 1; --j) acc = acc + (s_in[r + 12 - j][c] + s_in[r + 12 + j][c]) * kGauss[j];
+        s_v[r][c] = acc;
+    }
+    __syncthreads();
+    // axis 1: s_g[r][c] = column x0-1+c, s_v column index c+12
+    for (int e = tid; e < GR * GR; e += 256) {
+        const int r = e / GR, c = e - r * GR;
+        double acc = s_v[r][c + 12] * kGauss[0];
+        for (int j = 12; j >= 1; --j) acc = acc + (s_v[r][c + 12 - j] + s_v[r][c + 12 + j]) * kGauss[j];
+        s_g[r][c] = acc;
+    }
+    __syncthreads();
+    for (int e = tid; e < GT * GT; e += 256) {
+        const int r = e / GT, c = e - r * GT;
+        const int y = y0 + r, x = x0 + c;
+        if (y >= H || x >= W) continue;
+        const double v = s_g[r + 1][c + 1];
+        const double up = y > 0 ? s_g[r][c + 1] : 0.0;
+        const double dn = y < H - 1 ? s_g[r + 2][c + 1] : 0.0;
+        const double lf = x > 0 ? s_g[r + 1][c] : 0.0;
+        const double rt = x < W - 1 ? s_g[r + 1][c + 2] : 0.0;
+        if (v >= up && v >= dn && v >= lf && v >= rt && v > thre) {
+            const int slot = atomicAdd(cnt + np, 1);
+            if (slot < cap) list[(size_t)np * cap + slot] = y * W + x;
+        }
+    }
+}
+
+// One workgroup per frame: order each part's peaks row-major (np.nonzero), assign the
+// global running ids, write candidate rows (x, y, score, id) into the record.
+__global__ __launch_bounds__(256) void peaks_finalize(const int* __restrict__ cnt, const int* __restrict__ list,
+                                                      const double* __restrict__ avg, int H, int W, RecordLayout L,
+                                                      uint8_t* __restrict__ records, int* __restrict__ peak_pos,
+                                                      int* __restrict__ part_cnt) {
+    const int n = blockIdx.x;
+    const int cap = L.peaks_per_part;
+    __shared__ int s_cnt[18], s_start[18];
+    if (threadIdx.x == 0) {
+        int acc = 0, over = 0;
+        for (int p = 0; p < 18; ++p) {
+            int c = cnt[n * 18 + p];
+            if (c > cap) {
+                over = 1;
+                c = cap;
+            }
+            s_cnt[p] = c;
+            s_start[p] = acc;
+            acc += c;
+        }
+        int32_t* hdr = reinterpret_cast<int32_t*>(records + (size_t)n * L.bytes);
+        hdr[0] = over ? -5 : 0;
+        hdr[1] = acc;
+        hdr[2] = 0;
+        hdr[3] = 0;
+    }
+    __syncthreads();
+    double* cand = reinterpret_cast<double*>(records + (size_t)n * L.bytes + L.cand_off);
+    for (int p = 0; p < 18; ++p) {
+        const int c = s_cnt[p];
+        const int* lp = list + ((size_t)n * 18 + p) * cap;
+        for (int i = threadIdx.x; i < c; i += blockDim.x) {
+            const int v = lp[i];
+            int rank = 0;
+            for (int j = 0; j < c; ++j) rank += lp[j] < v;
+            const int y = v / W, x = v - y * W;
+            const int id = s_start[p] + rank;
+            double* row = cand + (size_t)id * 4;
+            row[0] = (double)x;
+            row[1] = (double)y;
+            row[2] = avg[(((size_t)n * 18 + p) * H + y) * W + x];
+            row[3] = (double)id;
+            peak_pos[((size_t)n * 18 + p) * cap + rank] = v;
+        }
+        if (threadIdx.x == 0) part_cnt[n * 18 + p] = c;
+    }
+}
+
+// grid (frames * 19 limbs, blocks per limb); pair (i, j) -> score[n][k][i*nB + j]
+// (-inf when criterion1/criterion2 fail; src/body.py:137-141).
+__global__ __launch_bounds__(256) void paf_score(PafScales S, const int* __restrict__ peak_pos,
+                                                 const int* __restrict__ part_cnt, int cap, double thre2,
+                                                 double* __restrict__ score) {
+    const int nk = blockIdx.x;
+    const int n = nk / 19, k = nk - n * 19;
+    const int pa = kLimbA[k], pb = kLimbB[k];
+    const int nA = part_cnt[n * 18 + pa], nB = part_cnt[n * 18 + pb];
+    const int total = nA * nB;
+    const int chx = kPafX[k];  // y component is channel chx + 1 (src/body.py:101-103)
+    const int* posA = peak_pos + ((size_t)n * 18 + pa) * cap;
+    const int* posB = peak_pos + ((size_t)n * 18 + pb) * cap;
+    double* out = score + (size_t)nk * cap * cap;
+    for (int e = blockIdx.y * blockDim.x + threadIdx.x; e < total; e += gridDim.y * blockDim.x) {
+        const int i = e / nB, j = e - i * nB;
+        const int va = posA[i], vb = posB[j];
+        const int ya = va / S.W, xa = va - ya * S.W;
+        const int yb = vb / S.W, xb = vb - yb * S.W;
+        const long long vx = xb - xa, vy = yb - ya;
+        const double norm = sqrt((double)(vx * vx + vy * vy)) + 1e-10;
+        const double ux = (double)vx / norm, uy = (double)vy / norm;
+        const double stx = ((double)xb - (double)xa) / 9.0;
+        const double sty = ((double)yb - (double)ya) / 9.0;
+        double acc = 0.0;
+        int above = 0;
+        for (int t = 0; t < 10; ++t) {
+            const double fx = t == 9 ? (double)xb : (double)t * stx + (double)xa;
+            const double fy = t == 9 ? (double)yb : (double)t * sty + (double)ya;
+            const int X = (int)rint(fx), Y = (int)rint(fy);
+            // paf_avg[Y, X, ch] = sum over scales of float32(resize(x8 map) / n_scales),
+            // accumulated in float64 (src/body.py:61-68); only the sampled pixels are
+            // ever evaluated, the full-resolution PAF maps are never materialised.
+            double px = 0.0, py = 0.0;
+            for (int s = 0; s < S.n; ++s) {
+                const size_t plane = (size_t)S.hs[s] * S.ws[s];
+                const float* mx = S.mid[s] + ((size_t)n * S.cm + chx) * plane;
+                float vx_, vy_;
+                if (S.hs[s] == S.H && S.ws[s] == S.W) {
+                    vx_ = mx[(size_t)Y * S.ws[s] + X];
+                    vy_ = mx[plane + (size_t)Y * S.ws[s] + X];
+                } else {
+                    const CubicTap ty = cubic_tap(Y, S.sy[s], S.hs[s]);
+                    const CubicTap tx = cubic_tap(X, S.sx[s], S.ws[s]);
+                    vx_ = cubic_sample_f32(mx, S.ws[s], ty, tx);
+                    vy_ = cubic_sample_f32(mx + plane, S.ws[s], ty, tx);
+                }
+                px = px + (double)(vx_ / (float)S.n);
+                py = py + (double)(vy_ / (float)S.n);
+            }
+            const double sm = px * ux + py * uy;
+            acc = acc + sm;
+            above += sm > thre2;
+        }
+        const double prior = 0.5 * (double)S.H / norm - 1.0;
+        const double sc = acc / 10.0 + (prior > 0.0 ? 0.0 : prior);
+        out[e] = (above > 8 && sc > 0.0) ? sc : -INFINITY;
+    }
+}
+
+// One workgroup per (frame, limb): greedy matching in the order of a stable descending
+// sort (ties -> smaller i*nB+j first), stopping at min(nA, nB) (src/body.py:143-151).
+__global__ __launch_bounds__(256) void limb_greedy(const double* __restrict__ score, const int* __restrict__ part_cnt,
+                                                   int cap, Conn* __restrict__ conn, int* __restrict__ conn_cnt) {
+    const int nk = blockIdx.x;
+    const int n = nk / 19, k = nk - n * 19;
+    const int nA = part_cnt[n * 18 + kLimbA[k]], nB = part_cnt[n * 18 + kLimbB[k]];
+    extern __shared__ unsigned char s_used[];  // [cap] A flags, [cap] B flags
+    __shared__ double s_bs[4];
+    __shared__ int s_bi[4];
+    __shared__ int s_count;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (nA == 0 || nB == 0) {
+        if (tid == 0) conn_cnt[nk] = -1;  // special_k (src/body.py:153-155)
+        return;
+    }
+    for (int i = tid; i < 2 * cap; i += 256) s_used[i] = 0;
+    if (tid == 0) s_count = 0;
+    __syncthreads();
+    const double* sc = score + (size_t)nk * cap * cap;
+    const int total = nA * nB, limit = nA < nB ? nA : nB;
+    Conn* out = conn + (size_t)nk * cap;
+    for (;;) {
+        double best = -INFINITY;
+        int bidx = 0x7fffffff;
+        for (int e = tid; e < total; e += 256) {
+            const int i = e / nB, j = e - i * nB;
+            if (s_used[i] | s_used[cap + j]) continue;
+            const double v = sc[e];
+            if (v > best) {  // e increases per thread, so ties keep the smaller index
+                best = v;
+                bidx = e;
+            }
+        }
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double ob = __shfl_xor(best, off);
+            const int oi = __shfl_xor(bidx, off);
+            if (ob > best || (ob == best && oi < bidx)) {
+                best = ob;
+                bidx = oi;
+            }
+        }
+        if (lane == 0) {
+            s_bs[wave] = best;
+            s_bi[wave] = bidx;
+        }
+        __syncthreads();
+        best = s_bs[0];
+        bidx = s_bi[0];
+        for (int w = 1; w < 4; ++w)
+            if (s_bs[w] > best || (s_bs[w] == best && s_bi[w] < bidx)) {
+                best = s_bs[w];
+                bidx = s_bi[w];
+            }
+        if (bidx == 0x7fffffff || best == -INFINITY) break;
+        const int i = bidx / nB, j = bidx - i * nB;
+        const int c = s_count;
+        if (tid == 0) {
+            out[c].i = i;
+            out[c].j = j;
+            out[c].s = best;
+            s_used[i] = 1;
+            s_used[cap + j] = 1;
+            s_count = c + 1;
+        }
+        __syncthreads();
+        if (c + 1 >= limit) break;
+    }
+    __syncthreads();
+    if (tid == 0) conn_cnt[nk] = s_count;
+}
+
+// One wavefront per frame: sequential person assembly with lane-parallel row scans.
+__global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ conn, const int* __restrict__ conn_cnt,
+                                                      const int* __restrict__ part_cnt, RecordLayout L,
+                                                      uint8_t* __restrict__ records) {
+    extern __shared__ double s_sub[];  // [max_people][20]
+    const int n = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int cap = L.peaks_per_part, maxp = L.max_people;
+    uint8_t* rec = records + (size_t)n * L.bytes;
+    int32_t* hdr = reinterpret_cast<int32_t*>(rec);
+    const double* cand = reinterpret_cast<const double*>(rec + L.cand_off);
+    double* outsub = reinterpret_cast<double*>(rec + L.subset_off);
+    __shared__ int s_start[18];
+    if (lane < 18) {
+        int acc = 0;
+        for (int p = 0; p < lane; ++p) acc += part_cnt[n * 18 + p];
+        s_start[lane] = acc;
+    }
+    __syncthreads();
+    int status = hdr[0];
+    int nrows = 0;
+    for (int k = 0; k < 19 && status == 0; ++k) {
+        const int nc = conn_cnt[n * 19 + k];
+        if (nc < 0) continue;
+        const int ia = kLimbA[k], ib = kLimbB[k];
+        const Conn* ck = conn + ((size_t)n * 19 + k) * cap;
+        for (int c = 0; c < nc; ++c) {
+            const double idA = (double)(s_start[ia] + ck[c].i);
+            const double idB = (double)(s_start[ib] + ck[c].j);
+            const double s = ck[c].s;
+            int found = 0, j1 = -1, j2 = -1;
+            for (int r0 = 0; r0 < nrows; r0 += 64) {
+                const int r = r0 + lane;
+                const bool hit = r < nrows && (s_sub[r * 20 + ia] == idA || s_sub[r * 20 + ib] == idB);
+                unsigned long long b = __ballot(hit);
+                while (b && found < 3) {
+                    const int bit = __ffsll((long long)b) - 1;
+                    b &= b - 1;
+                    if (found == 0) j1 = r0 + bit;
+                    else if (found == 1) j2 = r0 + bit;
+                    ++found;
+                }
+            }
+            if (found > 2) {  // subset_idx[2] = j -> IndexError (src/body.py:173)
+                status = -6;
+                break;
+            }
+            if (found == 1) {
+                if (lane == 0 && s_sub[j1 * 20 + ib] != idB) {
+                    s_sub[j1 * 20 + ib] = idB;
+                    s_sub[j1 * 20 + 19] = s_sub[j1 * 20 + 19] + 1.0;
+                    s_sub[j1 * 20 + 18] = s_sub[j1 * 20 + 18] + (cand[(size_t)idB * 4 + 2] + s);
+                }
+            } else if (found == 2) {
+                const bool both = lane < 18 && s_sub[j1 * 20 + lane] >= 0.0 && s_sub[j2 * 20 + lane] >= 0.0;
+                if (__ballot(both) == 0ull) {  // disjoint: merge j2 into j1, drop j2
+                    if (lane < 18) s_sub[j1 * 20 + lane] = s_sub[j1 * 20 + lane] + (s_sub[j2 * 20 + lane] + 1.0);
+                    if (lane == 18 || lane == 19) s_sub[j1 * 20 + lane] = s_sub[j1 * 20 + lane] + s_sub[j2 * 20 + lane];
+                    __syncthreads();
+                    if (lane == 0) s_sub[j1 * 20 + 18] = s_sub[j1 * 20 + 18] + s;
+                    __syncthreads();
+                    for (int r = j2; r < nrows - 1; ++r) {
+                        double v = lane < 20 ? s_sub[(r + 1) * 20 + lane] : 0.0;
+                        __syncthreads();
+                        if (lane < 20) s_sub[r * 20 + lane] = v;
+                        __syncthreads();
+                    }
+                    --nrows;
+                } else if (lane == 0) {
+                    s_sub[j1 * 20 + ib] = idB;
+                    s_sub[j1 * 20 + 19] = s_sub[j1 * 20 + 19] + 1.0;
+                    s_sub[j1 * 20 + 18] = s_sub[j1 * 20 + 18] + (cand[(size_t)idB * 4 + 2] + s);
+                }
+            } else if (k < 17) {
+                if (nrows >= maxp) {
+                    status = -5;
+                    break;
+                }
+                if (lane < 20) {
+                    double v = -1.0;
+                    if (lane == ia) v = idA;
+                    if (lane == ib) v = idB;
+                    if (lane == 19) v = 2.0;
+                    if (lane == 18) v = (cand[(size_t)idA * 4 + 2] + cand[(size_t)idB * 4 + 2]) + s;
+                    s_sub[nrows * 20 + lane] = v;
+                }
+                ++nrows;
+            }
+            __syncthreads();
+        }
+    }
+    // prune (src/body.py:203-208) and emit in order
+    int kept = 0;
+    if (status == 0) {
+        for (int r = 0; r < nrows; ++r) {
+            const double cntp = s_sub[r * 20 + 19], tot = s_sub[r * 20 + 18];
+            const bool drop = cntp < 4.0 || tot / cntp < 0.4;
+            if (!drop) {
+                if (lane < 20) outsub[(size_t)kept * 20 + lane] = s_sub[r * 20 + lane];
+                ++kept;
+            }
+        }
+    }
+    if (lane == 0) {
+        hdr[0] = status;
+        hdr[2] = kept;
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+void launch_gauss_nms(const double* avg, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
+                      hipStream_t st) {
+    dim3 grid((W + GT - 1) / GT, (H + GT - 1) / GT, NP);
+    hipLaunchKernelGGL(gauss_nms, grid, dim3(256), 0, st, avg, 18, H, W, thre, cap, cnt, list);
+}
+
+void launch_peaks_finalize(const int* cnt, const int* list, const double* avg, int N, int H, int W,
+                           const RecordLayout& L, uint8_t* records, int* peak_pos, int* part_cnt, hipStream_t st) {
+    hipLaunchKernelGGL(peaks_finalize, dim3(N), dim3(256), 0, st, cnt, list, avg, H, W, L, records, peak_pos,
+                       part_cnt);
+}
+
+void launch_paf_score(const PafScales& S, const int* peak_pos, const int* part_cnt, int N, int cap, double thre2,
+                      double* score, hipStream_t st) {
+    int by = (cap * cap + 255) / 256;
+    if (by > 16) by = 16;
+    hipLaunchKernelGGL(paf_score, dim3(N * 19, by), dim3(256), 0, st, S, peak_pos, part_cnt, cap, thre2, score);
+}
+
+void launch_limb_greedy(const double* score, const int* part_cnt, int N, int cap, Conn* conn, int* conn_cnt,
+                        hipStream_t st) {
+    hipLaunchKernelGGL(limb_greedy, dim3(N * 19), dim3(256), 2 * cap, st, score, part_cnt, cap, conn, conn_cnt);
+}
+
+void launch_assemble(const Conn* conn, const int* conn_cnt, const int* part_cnt, int N, const RecordLayout& L,
+                     uint8_t* records, hipStream_t st) {
+    hipLaunchKernelGGL(assemble_people, dim3(N), dim3(64), sizeof(double) * 20 * L.max_people, st, conn, conn_cnt,
+                       part_cnt, L, records);
+}
+
+}  // namespace opose

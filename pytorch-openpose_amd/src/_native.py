@@ -1,0 +1,184 @@
+"""ctypes binding of libopose.so (the C ABI declared in include/opose.h).
+
+This is the only way the package computes anything: there is no CPU fallback.  If the
+shared library is missing or fails to load, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("OPOSE_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libopose.so"))
+
+OPOSE_OK = 0
+OPOSE_E_ARG, OPOSE_E_SHAPE, OPOSE_E_HIP, OPOSE_E_WEIGHTS, OPOSE_E_CAPACITY, OPOSE_E_ASSEMBLY = -1, -2, -3, -4, -5, -6
+NET_BODY, NET_HAND = 0, 1
+IN_DEVICE, OUT_DEVICE = 1, 2
+MAX_SCALES = 8
+
+
+class Params(C.Structure):
+    _fields_ = [("n_scales", C.c_int), ("scales", C.c_double * MAX_SCALES), ("boxsize", C.c_double),
+                ("stride", C.c_int), ("pad_value", C.c_int), ("thre1", C.c_double), ("thre2", C.c_double),
+                ("thre_hand", C.c_double)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libopose.so not found at {LIB_PATH}: build it with `make -C pytorch-openpose_amd` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    P, I, D, S = C.c_void_p, C.c_int, C.c_double, C.c_size_t
+    sig = {
+        "opose_default_params": (None, [I, C.POINTER(Params)]),
+        "opose_create": (I, [I, C.POINTER(P)]),
+        "opose_destroy": (None, [P]),
+        "opose_last_error": (C.c_char_p, [P]),
+        "opose_set_stream": (I, [P, P]),
+        "opose_get_stream": (P, [P]),
+        "opose_synchronize": (I, [P]),
+        "opose_set_capacity": (I, [P, I, I]),
+        "opose_body_record_bytes": (S, [P]),
+        "opose_load_weights": (I, [P, I, C.POINTER(P), P, I]),
+        "opose_body_forward": (I, [P, P, I, I, I, P, P, I]),
+        "opose_hand_forward": (I, [P, P, I, I, I, P, I]),
+        "opose_body_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, I]),
+        "opose_body_post": (I, [P, P, I, I, I, I, I, I, I, C.POINTER(Params), P, I]),
+        "opose_hand_infer": (I, [P, P, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, P, I]),
+        "opose_hand_post": (I, [P, C.POINTER(P), P, P, P, P, I, I, I, C.POINTER(Params), P, P, I]),
+        "opose_profile_enable": (I, [P, I]),
+        "opose_profile_reset": (I, [P]),
+        "opose_profile_read": (I, [P, C.c_char_p, S]),
+        "opose_debug_conv": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P]),
+        "opose_debug_preprocess": (I, [P, P, I, I, D, I, P, P]),
+        "opose_debug_heat": (I, [P, P, I, I, I, I, I, I, P, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _ = D
+    return lib
+
+
+lib = _load()
+
+EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last_error", "opose_set_stream",
+            "opose_get_stream", "opose_synchronize", "opose_set_capacity", "opose_body_record_bytes",
+            "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_body_infer",
+            "opose_body_post", "opose_hand_infer", "opose_hand_post", "opose_profile_enable",
+            "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_preprocess",
+            "opose_debug_heat"]
+
+
+class OposeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libopose error {code}: {msg}")
+        self.code = code
+
+
+def default_params(net: int, **kw) -> Params:
+    p = Params()
+    lib.opose_default_params(net, C.byref(p))
+    if "scale_search" in kw and kw["scale_search"] is not None:
+        ss = list(kw.pop("scale_search"))
+        if not 1 <= len(ss) <= MAX_SCALES:
+            raise ValueError("scale_search must have 1..8 entries")
+        p.n_scales = len(ss)
+        for i, s in enumerate(ss):
+            p.scales[i] = float(s)
+    for k, v in kw.items():
+        if v is not None:
+            setattr(p, k, v)
+    return p
+
+
+def _ptr(a) -> int:
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return int(a.data_ptr())  # torch tensor
+
+
+class Handle:
+    """One device, one stream, weights + workspace (opose_t*)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        rc = lib.opose_create(int(device), C.byref(h))
+        if rc != OPOSE_OK:
+            raise OposeError(rc, "opose_create failed (no usable HIP device?)")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.opose_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc: int):
+        if rc != OPOSE_OK:
+            raise OposeError(rc, (lib.opose_last_error(self.h) or b"").decode())
+        return rc
+
+    # ---- configuration
+    def set_capacity(self, peaks_per_part: int, max_people: int):
+        self.check(lib.opose_set_capacity(self.h, peaks_per_part, max_people))
+
+    def record_bytes(self) -> int:
+        return int(lib.opose_body_record_bytes(self.h))
+
+    def set_stream(self, stream_ptr: int | None):
+        self.check(lib.opose_set_stream(self.h, stream_ptr or None))
+
+    def stream(self) -> int:
+        return lib.opose_get_stream(self.h) or 0
+
+    def synchronize(self):
+        self.check(lib.opose_synchronize(self.h))
+
+    # ---- weights
+    def load_weights(self, net: int, tensors):
+        """tensors: list of float32 C-contiguous numpy arrays in reference state_dict order."""
+        arrs = [np.ascontiguousarray(t, dtype=np.float32) for t in tensors]
+        ptrs = (C.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+        shapes = np.ones((len(arrs), 4), np.int64)
+        for i, a in enumerate(arrs):
+            shapes[i, :a.ndim] = a.shape
+        self.check(lib.opose_load_weights(self.h, net, ptrs, shapes.ctypes.data, len(arrs)))
+
+    # ---- profiling
+    def profile(self, enable: bool):
+        self.check(lib.opose_profile_enable(self.h, int(enable)))
+
+    def profile_reset(self):
+        self.check(lib.opose_profile_reset(self.h))
+
+    def profile_read(self) -> dict:
+        import json
+        buf = C.create_string_buffer(1 << 16)
+        self.check(lib.opose_profile_read(self.h, buf, len(buf)))
+        return json.loads(buf.value.decode())
+
+
+def decode_record(rec: np.ndarray, peaks_per_part: int, max_people: int):
+    """One Body record (uint8 view) -> (status, candidate, subset) in the reference's dtypes."""
+    hdr = rec[:16].view(np.int32)
+    status, n_cand, n_people = int(hdr[0]), int(hdr[1]), int(hdr[2])
+    cap_c = 18 * peaks_per_part
+    cand = rec[16:16 + 32 * cap_c].view(np.float64).reshape(cap_c, 4)[:n_cand].copy()
+    off = 16 + 32 * cap_c
+    sub = rec[off:off + 160 * max_people].view(np.float64).reshape(max_people, 20)[:n_people].copy()
+    if n_cand == 0:
+        cand = np.array([])          # np.array([]) in the reference when no peak exists (src/body.py:160)
+    if n_people == 0:
+        sub = -1 * np.ones((0, 20))  # src/body.py:159
+    return status, cand, sub

@@ -1,0 +1,133 @@
+"""Body pose estimation with the reference's call surface (hitmaxiang/pytorch-openpose src/body.py).
+
+    body = Body('body_pose_model.pth')
+    candidate, subset = body(oriImg)          # oriImg: uint8 H x W x 3, BGR
+
+Returns exactly what `Body.__call__` (src/body.py:24-212) returns:
+* candidate: float64 [N, 4] rows (x, y, score, id), or shape (0,) when no peak exists;
+* subset:    float64 [P, 20]: candidate ids per part (-1 = missing), total score, part count.
+
+Everything after weight loading runs on the GPU in libopose: uint8 cubic resize + pad +
+normalise, the VGG-19/CPM network (implicit-GEMM fp32 MFMA), x8 cubic upsample, resize
+and scale averaging, Gaussian(sigma=3) peak NMS, PAF line integrals, greedy matching and
+person assembly.  Only the fixed-size per-frame record crosses PCIe.
+
+Extras beyond the reference (defaults = reference values, src/body.py:25-31):
+scale_search, boxsize, stride, padValue, thre1, thre2, device; `Body.batch(frames)` runs
+a video batch through one launch sequence; `Body.infer_records` keeps inputs/outputs on
+the device (multi-GPU gather, benchmark).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _native, util
+from .model import bodypose_model
+
+
+def _load_state(model_path):
+    if isinstance(model_path, dict):
+        return model_path
+    import torch
+    return torch.load(model_path, map_location="cpu", weights_only=True)
+
+
+class Body(object):
+    def __init__(self, model_path, device: int = 0, scale_search=(0.5,), boxsize=368, stride=8, padValue=128,
+                 thre1=0.1, thre2=0.05, peaks_per_part=128, max_people=96):
+        self.model = bodypose_model(device)
+        model_dict = util.transfer(self.model, _load_state(model_path))
+        self.model.load_state_dict(model_dict)
+        self.model.eval()
+        self.handle = self.model.handle
+        self.params = _native.default_params(_native.NET_BODY, scale_search=scale_search, boxsize=float(boxsize),
+                                             stride=int(stride), pad_value=int(padValue), thre1=float(thre1),
+                                             thre2=float(thre2))
+        self.peaks_per_part, self.max_people = peaks_per_part, max_people
+        self.handle.set_capacity(peaks_per_part, max_people)
+
+    # ------------------------------------------------------------------ host API
+    def __call__(self, oriImg):
+        return self.batch(oriImg[None])[0]
+
+    def batch(self, frames):
+        """frames: uint8 [N, H, W, 3] (or a list of equally sized frames) -> list of (candidate, subset)."""
+        if isinstance(frames, (list, tuple)):
+            frames = np.stack(frames)
+        frames = np.asarray(frames)
+        if frames.dtype != np.uint8 or frames.ndim != 4 or frames.shape[3] != 3:
+            raise ValueError("expected uint8 frames [N, H, W, 3]")
+        if not (frames.strides[3] == 1 and frames.strides[2] == 3 and frames.strides[1] > 0
+                and frames.strides[0] >= frames.strides[1] * frames.shape[1]):
+            frames = np.ascontiguousarray(frames)
+        N, H, W, _ = frames.shape
+        while True:
+            rb = self.handle.record_bytes()
+            rec = np.empty((N, rb), np.uint8)
+            rc = _native.lib.opose_body_infer(self.handle.h, frames.ctypes.data, N, H, W, frames.strides[1],
+                                              frames.strides[0], self.params, rec.ctypes.data, 0)
+            if rc == _native.OPOSE_E_CAPACITY and self._grow():
+                continue
+            if rc not in (_native.OPOSE_OK, _native.OPOSE_E_CAPACITY, _native.OPOSE_E_ASSEMBLY):
+                self.handle.check(rc)
+            return [self._decode(r) for r in rec]
+
+    def post(self, maps, pad, H, W):
+        """Post-network path only (src/body.py:52-212) on one scale.
+
+        maps: float32 [N, 57, h, w] (PAF channels 0..37, heat 38..56); pad: util.padRightDownCorner pad."""
+        maps = np.ascontiguousarray(maps, dtype=np.float32)
+        N, c, hl, wl = maps.shape
+        assert c == 57
+        while True:
+            rec = np.empty((N, self.handle.record_bytes()), np.uint8)
+            rc = _native.lib.opose_body_post(self.handle.h, maps.ctypes.data, N, hl, wl, int(pad[2]), int(pad[3]),
+                                             int(H), int(W), self.params, rec.ctypes.data, 0)
+            if rc == _native.OPOSE_E_CAPACITY and self._grow():
+                continue
+            if rc not in (_native.OPOSE_OK, _native.OPOSE_E_CAPACITY, _native.OPOSE_E_ASSEMBLY):
+                self.handle.check(rc)
+            return [self._decode(r) for r in rec]
+
+    # ------------------------------------------------------------------ device API
+    def infer_records(self, frames_dev, records_dev=None):
+        """frames_dev: torch.uint8 cuda [N,H,W,3]; returns a torch.uint8 cuda [N, record_bytes] tensor.
+
+        Asynchronous on the handle's stream (no host synchronisation)."""
+        import torch
+        N, H, W, _ = frames_dev.shape
+        rb = self.handle.record_bytes()
+        if records_dev is None:
+            records_dev = torch.empty((N, rb), dtype=torch.uint8, device=frames_dev.device)
+        rc = _native.lib.opose_body_infer(self.handle.h, frames_dev.data_ptr(), N, H, W, frames_dev.stride(1),
+                                          frames_dev.stride(0), self.params, records_dev.data_ptr(),
+                                          _native.IN_DEVICE | _native.OUT_DEVICE)
+        self.handle.check(rc)
+        return records_dev
+
+    def decode_records(self, records):
+        """uint8 [N, record_bytes] (numpy or torch) -> list of (candidate, subset)."""
+        if hasattr(records, "cpu"):
+            records = records.cpu().numpy()
+        return [self._decode(r) for r in np.asarray(records)]
+
+    # ------------------------------------------------------------------ helpers
+    def _grow(self) -> bool:
+        if self.peaks_per_part >= 1024 and self.max_people >= 256:
+            return False
+        self.peaks_per_part = min(1024, self.peaks_per_part * 2)
+        self.max_people = min(256, self.max_people * 2)
+        self.handle.set_capacity(self.peaks_per_part, self.max_people)
+        return True
+
+    def _decode(self, rec):
+        status, cand, subset = _native.decode_record(rec, self.peaks_per_part, self.max_people)
+        if status == _native.OPOSE_E_ASSEMBLY:
+            # the reference raises here when a third subset row matches (src/body.py:170-173)
+            raise IndexError("list assignment index out of range")
+        if status == _native.OPOSE_E_CAPACITY:
+            raise RuntimeError("libopose: per-frame capacity exceeded (peaks_per_part=%d, max_people=%d)"
+                               % (self.peaks_per_part, self.max_people))
+        if status != 0:
+            raise _native.OposeError(status, "frame failed")
+        return cand, subset
