@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-iters", type=int, default=10)
+    ap.add_argument("--detail", action="store_true", help="per-layer kernel times to stderr")
     return ap.parse_args()
 
 
@@ -51,7 +52,8 @@ def cpu_baseline(frames_np, seconds):
     """Oracle (test infrastructure, used only as the timed CPU baseline) on whole frames."""
     from oracle import body_post, network
     from src.weights import BENCH_OUT_SCALE
-    threads = os.cpu_count() or 1
+    # the box's CPU share for one GPU (OMP_NUM_THREADS is set to it there), not the whole machine
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     sd = network.seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE)
 
@@ -111,7 +113,7 @@ def main():
     statuses = rec.view(torch.int32)[:, 0].cpu().numpy()
     counts = rec.view(torch.int32)[:, 1:3].cpu().numpy()
 
-    body.handle.profile(True)
+    body.handle.profile(2 if args.detail else 1)
     body.handle.profile_reset()
     if world > 1:
         torch.distributed.barrier()
@@ -126,6 +128,12 @@ def main():
     dt = time.perf_counter() - t0
     prof = body.handle.profile_read()
     body.handle.profile(False)
+    if args.detail and rank == 0:
+        det = sorted(((k, v) for k, v in prof.items() if k.startswith("layer/")), key=lambda kv: -kv[1]["ms"])
+        for k, v in det:
+            tf = v["flops"] / (v["ms"] * 1e-3) / 1e12 if v["ms"] else 0
+            print(f"{k:70s} {v['ms'] / args.steps:8.3f} ms/step {tf:7.1f} TF/s", file=sys.stderr)
+        prof = {k: v for k, v in prof.items() if not k.startswith("layer/")}
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

@@ -98,10 +98,10 @@ def seeded_state_dict(net: str, seed: int = 0, out_scale: dict | None = None):
         fan_in = cin * k * k
         w = rng.standard_normal((cout, cin, k, k), dtype=np.float32) * np.float32(np.sqrt(2.0 / fan_in))
         b = rng.standard_normal((cout,), dtype=np.float32) * np.float32(0.01)
-        if out_scale and name in out_scale:
-            wm, ba = out_scale[name]
-            w = w * np.float32(wm)
-            b = b + np.float32(ba)
+        if out_scale and name in out_scale:  # per-output-channel (or scalar) w*wm, b*wm + ba
+            wm, ba = (np.asarray(v, np.float32) for v in out_scale[name])
+            w = (w * (wm.reshape(-1, 1, 1, 1) if wm.ndim else wm)).astype(np.float32)
+            b = (b * wm + ba).astype(np.float32)
         sd[name + ".weight"] = torch.from_numpy(np.ascontiguousarray(w))
         sd[name + ".bias"] = torch.from_numpy(np.ascontiguousarray(b))
     return sd

@@ -27,6 +27,7 @@ namespace opose {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));  // native vector (HIP's float4 class defeats SROA)
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 constexpr int KC = 32;   // k rows per chunk
 constexpr int NT = 256;  // threads per workgroup
@@ -40,7 +41,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
     constexpr int RW = KC / 4;              // k rows loaded per wave per chunk
     constexpr int A_SZ = KC * MT, B_SZ = KC * PT;
 
-    __shared__ __attribute__((aligned(16))) float lds[2 * (A_SZ + B_SZ)];
+    __shared__ __attribute__((aligned(16))) float lds[2 * (A_SZ + B_SZ) + MT];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -55,21 +56,29 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
     const int p0 = blockIdx.x * PT;
     const int m0 = blockIdx.y * MT;
     const int HW = a.H * a.W;
+    float* s_bias = lds + 2 * (A_SZ + B_SZ);
+    if (tid < MT) s_bias[tid] = (m0 + tid < G.cout) ? G.bias[m0 + tid] : 0.f;
 
-    // ---- per-lane pixel state for the im2col gather
-    const float* pb[PJ];
+    // ---- per-lane pixel state for the im2col gather.  The activation is read through a
+    // buffer resource: an invalid (zero-padding) tap gets voffset 0xffffffff, which the
+    // hardware range check turns into 0.0f -> the gather is branch free.
+    const float* in_base = G.in + (size_t)G.in_coff * HW;
+    const int32_t* ib32 = reinterpret_cast<const int32_t*>(&in_base);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)in_base, (short)0, (int)0xffffff00u, 0x00020000);
+    (void)ib32;
+    uint32_t poff[PJ];  // element offset of the lane's pixel (channel 0 of its frame)
     int py[PJ], px[PJ];
-    bool pv[PJ];
 #pragma unroll
     for (int j = 0; j < PJ; ++j) {
         int p = p0 + j * 64 + lane;
-        pv[j] = p < a.npix;
-        int pc = pv[j] ? p : 0;
+        const bool v = p < a.npix;
+        int pc = v ? p : 0;
         int n = pc / HW;
         int r = pc - n * HW;
-        py[j] = r / a.W;
-        px[j] = r - py[j] * a.W;
-        pb[j] = G.in + ((size_t)n * G.in_cstride + G.in_coff) * HW + r;
+        py[j] = v ? r / a.W : -100000;  // out-of-range row => every tap invalid
+        px[j] = r - (r / a.W) * a.W;
+        poff[j] = (uint32_t)(n * G.in_cstride * HW + r);
     }
 
     const int nchunks = a.Kpad / KC;
@@ -97,10 +106,10 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
             ra[i] = *reinterpret_cast<const f32x4*>(G.wt + (size_t)(k0 + row) * a.Mpad + m0 + c4 * 4);
         }
         const int kw0 = __builtin_amdgcn_readfirstlane(k0 + wave * RW);
+        const i32x8 codes = *reinterpret_cast<const i32x8*>(ktab + kw0);  // wave-uniform
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
-            const int code = ktab[kw0 + r];  // wave-uniform: (c << 8) | (ky << 4) | kx, -1 = pad
-            const bool kv = code >= 0;
+            const int code = codes[r];  // (c << 8) | (ky << 4) | kx ; K padding rows carry zero weights
             const int cch = code >> 8;
             const int dy = ((code >> 4) & 15) - a.pad;
             const int dx = (code & 15) - a.pad;
@@ -108,8 +117,9 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
 #pragma unroll
             for (int j = 0; j < PJ; ++j) {
                 const int iy = py[j] + dy, ix = px[j] + dx;
-                const bool ok = kv && pv[j] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-                rb[r][j] = ok ? pb[j][delta] : 0.f;
+                const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+                const uint32_t off = ok ? (poff[j] + (uint32_t)delta) * 4u : 0xffffffffu;
+                rb[r][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
             }
         }
     };
@@ -141,21 +151,29 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
             const int buf = (c - c_begin) & 1;
             const bool more = c + 1 < c_end;
             if (more) load_chunk(c + 1);
-            const float* As = lds + buf * (A_SZ + B_SZ);
-            const float* Bs = As + A_SZ;
+            const float* As = lds + buf * (A_SZ + B_SZ) + wm0 + l31;
+            const float* Bs = lds + buf * (A_SZ + B_SZ) + A_SZ + wp0 + l31;
+            // fragments of k-step ks+1 are read while the MFMAs of k-step ks run
+            float av[2][TM], bv[2][TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) av[0][i] = As[hk * MT + i * 32];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bv[0][j] = Bs[hk * PT + j * 32];
 #pragma unroll
             for (int ks = 0; ks < KC / 2; ++ks) {
-                const int kr = 2 * ks + hk;
-                float av[TM], bv[TN];
+                const int cur = ks & 1, nxt = cur ^ 1;
+                if (ks + 1 < KC / 2) {
+                    const int kr = 2 * (ks + 1) + hk;
 #pragma unroll
-                for (int i = 0; i < TM; ++i) av[i] = As[kr * MT + wm0 + i * 32 + l31];
+                    for (int i = 0; i < TM; ++i) av[nxt][i] = As[kr * MT + i * 32];
 #pragma unroll
-                for (int j = 0; j < TN; ++j) bv[j] = Bs[kr * PT + wp0 + j * 32 + l31];
+                    for (int j = 0; j < TN; ++j) bv[nxt][j] = Bs[kr * PT + j * 32];
+                }
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
             }
             if (more) store_chunk(buf ^ 1);
             __syncthreads();
@@ -188,7 +206,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
                 if (m < G.cout) {
-                    float v = acc[i][j][r] + G.bias[m];
+                    float v = acc[i][j][r] + s_bias[m - m0];
                     if (G.relu) v = fmaxf(v, 0.f);
                     ob[(size_t)m * HW] = v;
                     if (ob2) ob2[(size_t)m * HW] = v;

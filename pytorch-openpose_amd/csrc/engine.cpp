@@ -130,6 +130,7 @@ struct DevConv {
 
 struct ProfEntry {
     std::string cls;
+    std::string detail;  // optional second aggregation key (per layer / tile choice)
     double flops;
     double bytes;
     hipEvent_t e0, e1;
@@ -156,6 +157,7 @@ struct opose_ctx {
         score, conn, conn_cnt, records, maps_in;
     // profiling
     bool prof = false;
+    bool detail = false;  // per-layer aggregation (opose_profile_enable(h, 2))
     std::vector<ProfEntry> pending;
     std::map<std::string, ProfAgg> agg;
     std::vector<hipEvent_t> event_pool;
@@ -189,11 +191,14 @@ struct opose_ctx {
             OPOSE_HIP_CHECK(hipEventSynchronize(pe.e1));
             float ms = 0;
             OPOSE_HIP_CHECK(hipEventElapsedTime(&ms, pe.e0, pe.e1));
-            auto& a = agg[pe.cls];
-            a.count++;
-            a.ms += ms;
-            a.flops += pe.flops;
-            a.bytes += pe.bytes;
+            for (const std::string* key : {&pe.cls, &pe.detail}) {
+                if (key->empty() || (key == &pe.detail && !detail)) continue;
+                auto& a = agg[*key];
+                a.count++;
+                a.ms += ms;
+                a.flops += pe.flops;
+                a.bytes += pe.bytes;
+            }
             event_pool.push_back(pe.e0);
             event_pool.push_back(pe.e1);
         }
@@ -282,7 +287,7 @@ static void upload_conv(opose_ctx* h, int net, const std::string& key, const std
         }
         m0 += parts[i]->cout;
     }
-    std::vector<int> ktab(dc->Kpad, -1);
+    std::vector<int> ktab(dc->Kpad, 0);  // padding rows: any in-range tap (weights are 0)
     for (int k = 0; k < dc->K; ++k) {
         int c = k / (dc->ks * dc->ks), r = k % (dc->ks * dc->ks);
         ktab[k] = (c << 8) | ((r / dc->ks) << 4) | (r % dc->ks);
@@ -344,6 +349,9 @@ static void run_conv(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W
     for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)a.K * a.npix;
     ProfEntry pe;
     h->prof_begin(pe, conv_class(c0->ks), flops, 0);
+    if (h->detail)
+        pe.detail = "layer/" + c0->name + "/" + std::to_string(t.mt) + "x" + std::to_string(t.pt) + "s" +
+                    std::to_string(t.splits) + "/n" + std::to_string(a.npix);
     launch_conv(a, ng, c0->ktab, t.mt, t.pt, h->stream);
     h->prof_end(pe);
 }
@@ -913,6 +921,7 @@ int opose_debug_heat(opose_t* h, const float* maps, int hl, int wl, int pad_down
 int opose_profile_enable(opose_t* h, int enable) {
     if (!h) return OPOSE_E_ARG;
     h->prof = enable != 0;
+    h->detail = enable >= 2;
     return OPOSE_OK;
 }
 
@@ -932,7 +941,7 @@ int opose_profile_read(opose_t* h, char* buf, size_t len) {
     std::string s = "{";
     bool first = true;
     for (auto& kv : h->agg) {
-        char tmp[256];
+        char tmp[512];
         std::snprintf(tmp, sizeof tmp, "%s\"%s\":{\"count\":%ld,\"ms\":%.6f,\"flops\":%.6e,\"bytes\":%.6e}",
                       first ? "" : ",", kv.first.c_str(), kv.second.count, kv.second.ms, kv.second.flops,
                       kv.second.bytes);

@@ -164,7 +164,7 @@ class Handle:
 
     def profile_read(self) -> dict:
         import json
-        buf = C.create_string_buffer(1 << 16)
+        buf = C.create_string_buffer(1 << 20)
         self.check(lib.opose_profile_read(self.h, buf, len(buf)))
         return json.loads(buf.value.decode())
 

@@ -57,15 +57,16 @@ class Body(object):
         frames = np.asarray(frames)
         if frames.dtype != np.uint8 or frames.ndim != 4 or frames.shape[3] != 3:
             raise ValueError("expected uint8 frames [N, H, W, 3]")
-        if not (frames.strides[3] == 1 and frames.strides[2] == 3 and frames.strides[1] > 0
-                and frames.strides[0] >= frames.strides[1] * frames.shape[1]):
+        if not (frames.strides[3] == 1 and frames.strides[2] == 3 and frames.strides[1] >= 3 * frames.shape[2]
+                and (frames.shape[0] == 1 or frames.strides[0] >= frames.strides[1] * frames.shape[1])):
             frames = np.ascontiguousarray(frames)
         N, H, W, _ = frames.shape
+        frame_stride = frames.strides[0] if N > 1 else frames.strides[1] * H
         while True:
             rb = self.handle.record_bytes()
             rec = np.empty((N, rb), np.uint8)
             rc = _native.lib.opose_body_infer(self.handle.h, frames.ctypes.data, N, H, W, frames.strides[1],
-                                              frames.strides[0], self.params, rec.ctypes.data, 0)
+                                              frame_stride, self.params, rec.ctypes.data, 0)
             if rc == _native.OPOSE_E_CAPACITY and self._grow():
                 continue
             if rc not in (_native.OPOSE_OK, _native.OPOSE_E_CAPACITY, _native.OPOSE_E_ASSEMBLY):

@@ -13,10 +13,20 @@ import numpy as np
 
 from .model import conv_specs
 
-# Bench calibration: a negative bias on the final heat-map conv so that the random-weight
-# network yields a sparse, person-like number of peaks (tens per part) instead of a dense
-# carpet.  Timing of the convolutions is value independent.
-BENCH_OUT_SCALE = {"Mconv7_stage6_L2": (1.0, 0.0)}
+# Bench calibration of the two output convs (timing of the convolutions is value independent):
+# * heat (Mconv7_stage6_L2): per-channel affine map sending each channel's 95th percentile of
+#   pre-activations on a uniform-noise 368x656 frame to 0 and its max to 1, so the seeded
+#   network yields ~17 peaks per part instead of a dense carpet of ~75;
+# * PAF (Mconv7_stage6_L1): +0.8 on every channel so that PAF vectors are coherent enough for
+#   limbs to connect (~20 assembled people per frame: a crowded-scene workload).
+BENCH_OUT_SCALE = {
+    "Mconv7_stage6_L2": (
+        [4.278, 4.923, 3.501, 1.921, 3.771, 5.688, 3.714, 3.656, 2.007, 3.603, 2.861, 4.452, 3.519, 4.595,
+         6.164, 3.614, 3.665, 2.856, 2.23],
+        [-3.625, -2.142, 0.815, -1.009, -0.328, -4.451, -2.318, -0.451, -1.747, -2.233, 0.418, -1.766, 0.657,
+         -6.417, -5.763, -0.264, -0.099, -1.635, 1.118]),
+    "Mconv7_stage6_L1": (1.0, 0.8),
+}
 
 
 def seeded_state_dict(net: str = "body", seed: int = 0, out_scale: dict | None = None, as_torch: bool = False):
@@ -26,10 +36,10 @@ def seeded_state_dict(net: str = "body", seed: int = 0, out_scale: dict | None =
         fan_in = cin * k * k
         w = rng.standard_normal((cout, cin, k, k), dtype=np.float32) * np.float32(np.sqrt(2.0 / fan_in))
         b = rng.standard_normal((cout,), dtype=np.float32) * np.float32(0.01)
-        if out_scale and name in out_scale:
-            wm, ba = out_scale[name]
-            w = w * np.float32(wm)
-            b = b + np.float32(ba)
+        if out_scale and name in out_scale:  # per-output-channel (or scalar) w*wm, b*wm + ba
+            wm, ba = (np.asarray(v, np.float32) for v in out_scale[name])
+            w = (w * (wm.reshape(-1, 1, 1, 1) if wm.ndim else wm)).astype(np.float32)
+            b = (b * wm + ba).astype(np.float32)
         sd[name + ".weight"] = np.ascontiguousarray(w)
         sd[name + ".bias"] = np.ascontiguousarray(b)
     if as_torch:

@@ -173,9 +173,13 @@ def test_network_full_size_and_batch_vs_oracle():
     rp, rh = onet.body_forward(torch.from_numpy(x[:1]), onet.seeded_state_dict("body", 0))
     _net_tol(paf[:1], rp.numpy())
     _net_tol(heat[:1], rh.numpy())
-    # batching: frame 0 alone equals frame 0 in a batch of 3 (bit-exact: same kernels, same order)
+    # batching: frame 0 alone vs inside a batch of 3 (tile / split-K choices depend on the batch,
+    # so the fp32 summation order may differ; the network tolerance applies)
     p1, h1 = m(x[:1])
-    assert np.array_equal(p1, paf[:1]) or np.abs(p1 - paf[:1]).max() <= 1e-6 * np.abs(p1).max()
+    _net_tol(p1, paf[:1])
+    _net_tol(h1, heat[:1])
+    p2, _ = m(x[2:3])
+    _net_tol(p2, paf[2:3])
 
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "body_e2e_*.npz"))), ids=os.path.basename)
