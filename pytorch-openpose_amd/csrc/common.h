@@ -42,6 +42,7 @@ struct ConvArgs {
     int Cin, ks, pad;   // input channels, kernel size, padding
     int K, Kpad, Mpad;  // K = Cin*ks*ks
     int npix;           // N*H*W
+    int tap_major;      // K ordered (tap, channel) with Cin padded to 32 (else OIHW + ktab)
     int splits;         // split-K factor (gridDim.z = ngroups * splits)
     int chunks_per_split;
     float* partial;     // [ngroups][splits][Mpad][npix] when splits > 1

@@ -28,24 +28,30 @@ namespace opose {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));  // native vector (HIP's float4 class defeats SROA)
 typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 constexpr int KC = 32;   // k rows per chunk
 constexpr int NT = 256;  // threads per workgroup
 
-template <int MT, int PT>
+// TAP: K ordered (tap, channel) with Cin padded to a multiple of KC -> one bounds check per
+// pixel per chunk and a wave-uniform channel stride (all layers with Cin >= 32); otherwise K is
+// the OIHW flattening decoded through `ktab` (conv1_1: K = 27).
+template <int MT, int PT, bool TAP>
 __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* __restrict__ ktab) {
     constexpr int WM = MT / 2, WP = PT / 2;
     constexpr int TM = WM / 32, TN = WP / 32;
-    constexpr int A_F4 = MT * KC / 4 / NT;  // float4 A loads per thread per chunk
     constexpr int PJ = PT / 64;             // pixel columns per lane
-    constexpr int RW = KC / 4;              // k rows loaded per wave per chunk
+    constexpr int RW = KC / 4;              // k rows gathered per wave per chunk
     constexpr int A_SZ = KC * MT, B_SZ = KC * PT;
+    constexpr int A_PW = A_SZ / 256 / 4;    // 1-KiB A pieces per wave per chunk
 
+    // [2 stages][A tile KC x MT | B tile KC x PT] + bias; both tiles are filled by LDS-DMA
+    // (buffer/global_load ... lds): no register staging, no ds_write pass.
     __shared__ __attribute__((aligned(16))) float lds[2 * (A_SZ + B_SZ) + MT];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l31 = lane & 31, hk = lane >> 5;
 
     const int zg = blockIdx.z;
@@ -60,13 +66,11 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
     if (tid < MT) s_bias[tid] = (m0 + tid < G.cout) ? G.bias[m0 + tid] : 0.f;
 
     // ---- per-lane pixel state for the im2col gather.  The activation is read through a
-    // buffer resource: an invalid (zero-padding) tap gets voffset 0xffffffff, which the
-    // hardware range check turns into 0.0f -> the gather is branch free.
+    // buffer resource: an invalid (zero-padding) tap gets a byte offset >= num_records, which
+    // the hardware range check turns into 0.0f -> the gather is branch free.
     const float* in_base = G.in + (size_t)G.in_coff * HW;
-    const int32_t* ib32 = reinterpret_cast<const int32_t*>(&in_base);
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)in_base, (short)0, (int)0xffffff00u, 0x00020000);
-    (void)ib32;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)in_base, (short)0, (int)0x80000000u, 0x00020000);
     uint32_t poff[PJ];  // element offset of the lane's pixel (channel 0 of its frame)
     int py[PJ], px[PJ];
 #pragma unroll
@@ -93,23 +97,39 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    f32x4 ra[A_F4];
-    float rb[RW][PJ];
+    const uint32_t HW4 = (uint32_t)HW * 4u;
+    // per-chunk gather state (computed once per chunk)
+    uint32_t base[PJ];
+    int ch0 = 0;
 
-    auto load_chunk = [&](int c) __attribute__((always_inline)) {
-        const int k0 = c * KC;
+    auto chunk_setup = [&](int c) __attribute__((always_inline)) {
+        if constexpr (TAP) {
+            const int cpt = a.Kpad / (KC * a.ks * a.ks);  // chunks per tap (wave-uniform scalars)
+            const int tap = c / cpt;
+            ch0 = (c - tap * cpt) * KC + wave * RW;
+            const int ky = tap / a.ks;
+            const int dy = ky - a.pad, dx = tap - ky * a.ks - a.pad;
+            const int shift = dy * a.W + dx;
 #pragma unroll
-        for (int i = 0; i < A_F4; ++i) {
-            int idx = tid + i * NT;
-            int row = idx / (MT / 4);
-            int c4 = idx - row * (MT / 4);
-            ra[i] = *reinterpret_cast<const f32x4*>(G.wt + (size_t)(k0 + row) * a.Mpad + m0 + c4 * 4);
+            for (int j = 0; j < PJ; ++j) {
+                const int iy = py[j] + dy, ix = px[j] + dx;
+                const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+                // invalid taps start at 3 GiB: every row offset stays >= 2 GiB = num_records -> 0.0f
+                base[j] = ok ? (poff[j] + (uint32_t)shift) * 4u : 0xC0000000u;
+            }
         }
-        const int kw0 = __builtin_amdgcn_readfirstlane(k0 + wave * RW);
-        const i32x8 codes = *reinterpret_cast<const i32x8*>(ktab + kw0);  // wave-uniform
+    };
+    // issue the LDS-DMA of B row r (this wave's) of chunk c into stage `buf`
+    auto dma_b_row = [&](int c, int buf, int r) __attribute__((always_inline)) {
+        float* Bs = lds + buf * (A_SZ + B_SZ) + A_SZ + (wave * RW + r) * PT;
+        if constexpr (TAP) {
+            const int ch = min(ch0 + r, a.Cin - 1);  // padded channels: any valid address (weights are 0)
+            const uint32_t choff = (uint32_t)ch * HW4;
 #pragma unroll
-        for (int r = 0; r < RW; ++r) {
-            const int code = codes[r];  // (c << 8) | (ky << 4) | kx ; K padding rows carry zero weights
+            for (int j = 0; j < PJ; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + j * 64), 4, base[j] + choff, 0, 0, 0);
+        } else {
+            const int code = ktab[c * KC + wave * RW + r];  // (c << 8) | (ky << 4) | kx
             const int cch = code >> 8;
             const int dy = ((code >> 4) & 15) - a.pad;
             const int dx = (code & 15) - a.pad;
@@ -118,42 +138,44 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
             for (int j = 0; j < PJ; ++j) {
                 const int iy = py[j] + dy, ix = px[j] + dx;
                 const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-                const uint32_t off = ok ? (poff[j] + (uint32_t)delta) * 4u : 0xffffffffu;
-                rb[r][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
+                const uint32_t off = ok ? (poff[j] + (uint32_t)delta) * 4u : 0xC0000000u;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + j * 64), 4, off, 0, 0, 0);
             }
         }
     };
-
-    auto store_chunk = [&](int buf) __attribute__((always_inline)) {
+    auto dma_a = [&](int c, int buf) __attribute__((always_inline)) {
+        const int k0 = c * KC;
         float* As = lds + buf * (A_SZ + B_SZ);
-        float* Bs = As + A_SZ;
 #pragma unroll
-        for (int i = 0; i < A_F4; ++i) {
-            int idx = tid + i * NT;
-            int row = idx / (MT / 4);
-            int c4 = idx - row * (MT / 4);
-            *reinterpret_cast<f32x4*>(As + row * MT + c4 * 4) = ra[i];
+        for (int i = 0; i < A_PW; ++i) {
+            const int piece = wave * A_PW + i;
+            const int f = piece * 256 + lane * 4;
+            const int row = f / MT, col = f - row * MT;
+            __builtin_amdgcn_global_load_lds((const void*)(G.wt + (size_t)(k0 + row) * a.Mpad + m0 + col),
+                                             (lds_ptr_t)(As + piece * 256), 16, 0, 0);
         }
-#pragma unroll
-        for (int r = 0; r < RW; ++r)
-#pragma unroll
-            for (int j = 0; j < PJ; ++j) Bs[(wave * RW + r) * PT + j * 64 + lane] = rb[r][j];
     };
 
     const int wm0 = (wave & 1) * WM;
     const int wp0 = (wave >> 1) * WP;
 
     if (c_begin < c_end) {
-        load_chunk(c_begin);
-        store_chunk(0);
-        __syncthreads();
+        chunk_setup(c_begin);
+        dma_a(c_begin, 0);
+#pragma unroll
+        for (int r = 0; r < RW; ++r) dma_b_row(c_begin, 0, r);
+        __syncthreads();  // s_waitcnt vmcnt(0) + barrier: stage 0 landed for every wave
         for (int c = c_begin; c < c_end; ++c) {
             const int buf = (c - c_begin) & 1;
             const bool more = c + 1 < c_end;
-            if (more) load_chunk(c + 1);
+            if (more) {
+                chunk_setup(c + 1);
+                dma_a(c + 1, buf ^ 1);
+            }
             const float* As = lds + buf * (A_SZ + B_SZ) + wm0 + l31;
             const float* Bs = lds + buf * (A_SZ + B_SZ) + A_SZ + wp0 + l31;
-            // fragments of k-step ks+1 are read while the MFMAs of k-step ks run
+            // fragments of k-step ks+1 are read while the MFMAs of k-step ks run; the next
+            // chunk's B rows are issued one per k-step, between this chunk's MFMAs
             float av[2][TM], bv[2][TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i) av[0][i] = As[hk * MT + i * 32];
@@ -169,14 +191,19 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
 #pragma unroll
                     for (int j = 0; j < TN; ++j) bv[nxt][j] = Bs[kr * PT + j * 32];
                 }
+                if (ks < RW && more) dma_b_row(c + 1, buf ^ 1, ks);
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
+                if (ks + 1 < KC / 2) {
+                    // keep the next step's LDS reads ahead of this step's MFMAs
+                    __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
+                }
             }
-            if (more) store_chunk(buf ^ 1);
-            __syncthreads();
+            __syncthreads();  // next stage landed everywhere; this stage free for reuse
         }
     }
 
@@ -255,7 +282,10 @@ __global__ __launch_bounds__(256) void maxpool2x2(const float* __restrict__ in, 
 template <int MT, int PT>
 static void launch_tile(const ConvArgs& a, int ngroups, const int* ktab, hipStream_t st) {
     dim3 grid((a.npix + PT - 1) / PT, a.Mpad / MT, ngroups * a.splits);
-    hipLaunchKernelGGL((conv_igemm_f32<MT, PT>), grid, dim3(NT), 0, st, a, ktab);
+    if (a.tap_major)
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true>), grid, dim3(NT), 0, st, a, ktab);
+    else
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, false>), grid, dim3(NT), 0, st, a, ktab);
 }
 
 void launch_conv(const ConvArgs& a, int ngroups, const int* ktab, int mt, int pt, hipStream_t st) {

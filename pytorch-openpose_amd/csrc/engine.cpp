@@ -118,6 +118,7 @@ struct DevBuf {
 struct DevConv {
     std::string name;
     int cin = 0, cout = 0, ks = 0, pad = 0, K = 0, Kpad = 0, Mpad = 0;
+    bool tap_major = false;  // K = (tap, channel padded to 32); see conv.hip
     float* wt = nullptr;
     float* bias = nullptr;
     int* ktab = nullptr;
@@ -273,7 +274,9 @@ static void upload_conv(opose_ctx* h, int net, const std::string& key, const std
     dc->ks = s0.ks;
     dc->pad = s0.pad;
     dc->K = s0.cin * s0.ks * s0.ks;
-    dc->Kpad = round_up(dc->K, 32);
+    dc->tap_major = s0.cin >= 32;
+    const int cin_pad = round_up(s0.cin, 32);
+    dc->Kpad = dc->tap_major ? s0.ks * s0.ks * cin_pad : round_up(dc->K, 32);
     int cout = 0;
     for (auto* p : parts) cout += p->cout;
     dc->cout = cout;
@@ -282,7 +285,12 @@ static void upload_conv(opose_ctx* h, int net, const std::string& key, const std
     int m0 = 0;
     for (size_t i = 0; i < parts.size(); ++i) {
         for (int m = 0; m < parts[i]->cout; ++m) {
-            for (int k = 0; k < dc->K; ++k) wt[(size_t)k * dc->Mpad + m0 + m] = w[i][(size_t)m * dc->K + k];
+            for (int k = 0; k < dc->K; ++k) {
+                // reference layout OIHW: k = c * ks*ks + tap
+                const int c = k / (s0.ks * s0.ks), tap = k % (s0.ks * s0.ks);
+                const int kk = dc->tap_major ? tap * cin_pad + c : k;
+                wt[(size_t)kk * dc->Mpad + m0 + m] = w[i][(size_t)m * dc->K + k];
+            }
             bias[m0 + m] = b[i][m];
         }
         m0 += parts[i]->cout;
@@ -318,6 +326,7 @@ static void run_conv(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W
     a.Kpad = c0->Kpad;
     a.Mpad = c0->Mpad;
     a.npix = N * H * W;
+    a.tap_major = c0->tap_major ? 1 : 0;
     DevConv* cs[2] = {c0, c1};
     Act ins[2] = {in0, in1}, outs[2] = {out0, out1};
     bool relus[2] = {relu0, relu1};
@@ -341,6 +350,9 @@ static void run_conv(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W
         a.g[0].out2_coff = dup.coff;
     }
     if (ng == 1) a.g[1] = a.g[0];
+    for (int g = 0; g < ng; ++g)  // the im2col gather addresses the input with 32-bit byte offsets
+        if ((double)N * ins[g].cstride * H * W * 4.0 >= 2147483648.0)
+            throw std::invalid_argument("activation slab >= 2 GiB: split the batch");
     const TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.Kpad / 32);
     a.splits = t.splits;
     a.chunks_per_split = t.cps;
@@ -851,6 +863,7 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
         ConvArgs a{};
         a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.ks = ks; a.pad = pad;
         a.K = c->K; a.Kpad = c->Kpad; a.Mpad = c->Mpad; a.npix = N * H * W;
+        a.tap_major = c->tap_major ? 1 : 0;
         ConvGroup& G = a.g[0];
         G.in = xd; G.in_cstride = Cin; G.in_coff = 0; G.wt = c->wt; G.bias = c->bias;
         G.out = yd; G.out_cstride = Cout; G.out_coff = 0; G.out2 = nullptr; G.cout = Cout; G.relu = relu;
