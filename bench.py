@@ -96,14 +96,16 @@ def main():
     frames = torch.from_numpy(frames_np).to(dev)
     rb = body.handle.record_bytes()
     rec = torch.empty((B, rb), dtype=torch.uint8, device=dev)
-    gathered = torch.empty((world * B, rb), dtype=torch.uint8, device=dev) if world > 1 else None
     lib_stream = torch.cuda.ExternalStream(body.handle.stream(), device=dev)
+    from src.dist import gather_records
 
     def step():
         body.infer_records(frames, rec)
         if world > 1:
+            # RCCL all_gather of the per-frame keypoint records, ordered after the library's
+            # kernels on its stream (src/dist.py)
             with torch.cuda.stream(lib_stream):
-                torch.distributed.all_gather_into_tensor(gathered, rec)
+                gather_records(rec, world * B, world)
 
     for _ in range(args.warmup):
         step()

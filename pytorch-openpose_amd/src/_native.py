@@ -169,6 +169,24 @@ class Handle:
         return json.loads(buf.value.decode())
 
 
+def record_bytes(peaks_per_part: int, max_people: int) -> int:
+    return 16 + 32 * 18 * peaks_per_part + 160 * max_people
+
+
+def encode_record(candidate, subset, peaks_per_part: int, max_people: int, status: int = 0) -> np.ndarray:
+    """Inverse of decode_record (host-side; used by tests and tools)."""
+    rec = np.zeros(record_bytes(peaks_per_part, max_people), np.uint8)
+    cand = np.asarray(candidate, np.float64).reshape(-1, 4)
+    sub = np.asarray(subset, np.float64).reshape(-1, 20)
+    if len(cand) > 18 * peaks_per_part or len(sub) > max_people:
+        raise ValueError("record capacity exceeded")
+    rec[:16].view(np.int32)[:3] = (status, len(cand), len(sub))
+    rec[16:16 + 32 * len(cand)].view(np.float64)[:] = cand.ravel()
+    off = 16 + 32 * 18 * peaks_per_part
+    rec[off:off + 160 * len(sub)].view(np.float64)[:] = sub.ravel()
+    return rec
+
+
 def decode_record(rec: np.ndarray, peaks_per_part: int, max_people: int):
     """One Body record (uint8 view) -> (status, candidate, subset) in the reference's dtypes."""
     hdr = rec[:16].view(np.int32)
