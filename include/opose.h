@@ -116,15 +116,16 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W,
 int opose_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int pad_down,
                     int pad_right, int H, int W, const opose_params* p, void* records, int flags);
 
-/* Hand on N square crops uint8 [S][S][3]: peaks [N][21][3] (x, y, score), found [N][21]
- * (0 = part missing, the reference's [0,0,0] row). */
-int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int S, int64_t row_stride,
+/* Hand on N crops uint8 [H][W][3] (util.handDetect gives squares): peaks [N][21][3]
+ * (x, y, score), found [N][21] (0 = part missing, the reference's [0,0,0] row). */
+int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride,
                      int64_t frame_stride, const opose_params* p, double* peaks,
                      int32_t* found, int flags);
 
-/* Post-network hand path: maps[s] = [N,22,hl[s],wl[s]] per scale s (pads per scale). */
+/* Post-network hand path: maps[s] = [N,22,hl[s],wl[s]] per scale s (pads per scale),
+ * crop H x W. */
 int opose_hand_post(opose_t* h, const float* const* maps, const int* hl, const int* wl,
-                    const int* pad_down, const int* pad_right, int n_scales, int N, int S,
+                    const int* pad_down, const int* pad_right, int n_scales, int N, int H, int W,
                     const opose_params* p, double* peaks, int32_t* found, int flags);
 
 /* ---- measurement ---------------------------------------------------------------------- */

@@ -155,7 +155,7 @@ struct opose_ctx {
     bool loaded[2] = {false, false};
     // workspace
     DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[kMaxScales], avg, cnt, list, peak_pos, part_cnt,
-        score, conn, conn_cnt, records, maps_in;
+        score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound;
     // profiling
     bool prof = false;
     bool detail = false;  // per-layer aggregation (opose_profile_enable(h, 2))
@@ -834,16 +834,105 @@ int opose_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int pa
     });
 }
 
-int opose_hand_infer(opose_t* h, const uint8_t*, int, int, int64_t, int64_t, const opose_params*, double*, int32_t*,
-                     int) {
-    if (h) h->err = "hand path not built yet";
-    return OPOSE_E_SHAPE;
+// Hand post path from per-scale x8 maps (mids[s] = [N][21][Hs][Ws]) to peaks / found.
+static void hand_post_common(opose_ctx* h, int N, int H, int W, const std::vector<ScaleGeom>& gs,
+                             const opose_params& p, double* peaks_out, int32_t* found_out, int flags) {
+    const int ns = (int)gs.size();
+    const int NP = N * 21;
+    double* avg = h->avg.ensure<double>((size_t)NP * H * W, h->stream);
+    ProfEntry pe;
+    for (int s = 0; s < ns; ++s) {
+        h->prof_begin(pe, "heat_full", 0, (double)NP * H * W * 8 * (s ? 2 : 1));
+        launch_heat_full(h->mids[s].ensure<float>(0, h->stream), 21, 0, 21, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy,
+                         gs[s].up_sx, ns, s > 0, avg, h->stream);
+        h->prof_end(pe);
+    }
+    int* lab = h->hlab.ensure<int>((size_t)NP * H * W, h->stream);
+    double* sums = h->hsums.ensure<double>((size_t)NP * H * W, h->stream);
+    int* cnt = h->cnt.ensure<int>((size_t)NP, h->stream);
+    double* pk = (flags & OPOSE_OUT_DEVICE) ? peaks_out : h->hpeaks.ensure<double>((size_t)NP * 3, h->stream);
+    int* fd = (flags & OPOSE_OUT_DEVICE) ? found_out : h->hfound.ensure<int>((size_t)NP, h->stream);
+    OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * NP, h->stream));
+    h->prof_begin(pe, "gauss_threshold", 0, (double)NP * H * W * 12);
+    launch_gauss_threshold(avg, NP, H, W, p.thre_hand, lab, cnt, h->stream);
+    h->prof_end(pe);
+    h->prof_begin(pe, "hand_cc", 0, 0);
+    launch_hand_cc(avg, NP, H, W, lab, sums, cnt, pk, fd, h->stream);
+    h->prof_end(pe);
+    if (!(flags & OPOSE_OUT_DEVICE)) {
+        OPOSE_HIP_CHECK(hipMemcpyAsync(peaks_out, pk, sizeof(double) * NP * 3, hipMemcpyDeviceToHost, h->stream));
+        OPOSE_HIP_CHECK(hipMemcpyAsync(found_out, fd, sizeof(int) * NP, hipMemcpyDeviceToHost, h->stream));
+        OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+    }
+    h->prof_drain();
 }
 
-int opose_hand_post(opose_t* h, const float* const*, const int*, const int*, const int*, const int*, int, int, int,
-                    const opose_params*, double*, int32_t*, int) {
-    if (h) h->err = "hand path not built yet";
-    return OPOSE_E_SHAPE;
+int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride, int64_t frame_stride,
+                     const opose_params* pp, double* peaks, int32_t* found, int flags) {
+    if (!h || !bgr || !peaks || !found || N <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
+    if (row_stride < (int64_t)W * 3 || frame_stride < row_stride * H) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const opose_params p = fill_params(pp, OPOSE_NET_HAND);
+        const uint8_t* fd = bgr;
+        if (!(flags & OPOSE_IN_DEVICE)) {
+            uint8_t* buf = h->frames.ensure<uint8_t>((size_t)frame_stride * N, h->stream);
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, (size_t)frame_stride * N, hipMemcpyHostToDevice, h->stream));
+            fd = buf;
+        }
+        std::vector<ScaleGeom> gs;
+        for (int s = 0; s < p.n_scales; ++s) gs.push_back(geom(p.scales[s], p, H, W));
+        for (int s = 0; s < p.n_scales; ++s) {
+            const ScaleGeom& g = gs[s];
+            float* x = h->x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
+            ProfEntry pe;
+            h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
+            launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp, g.Wp,
+                              (float)p.pad_value / 256.f - 0.5f, x, h->stream);
+            h->prof_end(pe);
+            float* Sb = hand_net(h, x, N, g.Hp, g.Wp);
+            upsample_to_mid(h, s, Sb, 150, N, g, 21);
+        }
+        hand_post_common(h, N, H, W, gs, p, peaks, found, flags & OPOSE_OUT_DEVICE);
+    });
+    return OPOSE_OK;
+}
+
+int opose_hand_post(opose_t* h, const float* const* maps, const int* hl, const int* wl, const int* pad_down,
+                    const int* pad_right, int n_scales, int N, int H, int W, const opose_params* pp,
+                    double* peaks, int32_t* found, int flags) {
+    if (!h || !maps || !hl || !wl || !pad_down || !pad_right || !peaks || !found || N <= 0 || H <= 0 || W <= 0 ||
+        n_scales < 1 || n_scales > OPOSE_MAX_SCALES)
+        return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        opose_params p = fill_params(pp, OPOSE_NET_HAND);
+        std::vector<ScaleGeom> gs;
+        for (int s = 0; s < n_scales; ++s) {
+            ScaleGeom g;
+            g.mult = 0;
+            g.hl = hl[s];
+            g.wl = wl[s];
+            g.Hp = 8 * hl[s];
+            g.Wp = 8 * wl[s];
+            g.Hs = g.Hp - pad_down[s];
+            g.Ws = g.Wp - pad_right[s];
+            if (g.Hs <= 0 || g.Ws <= 0) throw std::invalid_argument("bad pad");
+            g.up_sy = 1.0 / ((double)H / g.Hs);
+            g.up_sx = 1.0 / ((double)W / g.Ws);
+            const size_t n_in = (size_t)N * 22 * g.hl * g.wl;
+            const float* md = maps[s];
+            if (!(flags & OPOSE_IN_DEVICE)) {
+                float* buf = h->maps_in.ensure<float>(n_in, h->stream);
+                OPOSE_HIP_CHECK(hipMemcpyAsync(buf, maps[s], n_in * 4, hipMemcpyHostToDevice, h->stream));
+                md = buf;
+            }
+            upsample_to_mid(h, s, md, 22, N, g, 21);
+            gs.push_back(g);
+        }
+        hand_post_common(h, N, H, W, gs, p, peaks, found, flags & OPOSE_OUT_DEVICE);
+    });
+    return OPOSE_OK;
 }
 
 // ------------------------------------------------------------------ test hooks

@@ -34,6 +34,7 @@ void launch_heat_full(const float* mid, int Cm, int coff, int P, int N, int Hs, 
 // post.hip
 void launch_gauss_nms(const double* avg, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
                       hipStream_t st);
+void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st);
 void launch_peaks_finalize(const int* cnt, const int* list, const double* avg, int N, int H, int W,
                            const RecordLayout& L, uint8_t* records, int* peak_pos, int* part_cnt, hipStream_t st);
 void launch_paf_score(const PafScales& S, const int* peak_pos, const int* part_cnt, int N, int cap, double thre2,
@@ -42,5 +43,9 @@ void launch_limb_greedy(const double* score, const int* part_cnt, int N, int cap
                         hipStream_t st);
 void launch_assemble(const Conn* conn, const int* conn_cnt, const int* part_cnt, int N, const RecordLayout& L,
                      uint8_t* records, hipStream_t st);
+
+// hand.hip
+void launch_hand_cc(double* avg, int NP, int H, int W, int* lab, double* sums, const int* cnt, double* peaks,
+                    int* found, hipStream_t st);
 
 }  // namespace opose

@@ -40,53 +40,86 @@ constexpr int GT = 32;        // output tile (GT x GT)
 constexpr int GI = GT + 26;   // input tile incl. 13-pixel halo on each side
 constexpr int GR = GT + 2;    // smoothed rows/cols incl. the NMS ring
 
-// avg: [N*P][H][W] float64; one workgroup per GT x GT tile of one part of one frame.
-__global__ __launch_bounds__(256) void gauss_nms(const double* __restrict__ avg, int P, int H, int W, double thre,
-                                                 int cap, int* __restrict__ cnt, int* __restrict__ list) {
-    __shared__ double s_in[GI][GI];
-    __shared__ double s_v[GR][GI];
-    __shared__ double s_g[GR][GR];
-    const int tid = threadIdx.x;
-    const int x0 = blockIdx.x * GT, y0 = blockIdx.y * GT;
-    const int np = blockIdx.z;
-    const double* m = avg + (size_t)np * H * W;
+// Smooth one GT x GT tile (plus a 1-pixel ring) of one map into s_g (scipy order: axis 0
+// then axis 1, symmetric taps summed centre-first then |j| = 12 .. 1, float64, no FMA).
+struct GaussTile {
+    double in[GI][GI];
+    double v[GR][GI];
+    double g[GR][GR];
+};
 
+__device__ __forceinline__ void gauss_tile(const double* __restrict__ m, int H, int W, int x0, int y0, GaussTile& t) {
+    const int tid = threadIdx.x;
     for (int e = tid; e < GI * GI; e += 256) {
         const int r = e / GI, c = e - r * GI;
         const int gy = reflect_idx(y0 - 13 + r, H), gx = reflect_idx(x0 - 13 + c, W);
-        s_in[r][c] = m[(size_t)gy * W + gx];
+        t.in[r][c] = m[(size_t)gy * W + gx];
     }
     __syncthreads();
-    // axis 0 (scipy's first pass): s_v[r][c] = rows y0-1+r, input row index r+12
+    // axis 0 (scipy's first pass): v[r][c] = rows y0-1+r, input row index r+12
     for (int e = tid; e < GR * GI; e += 256) {
         const int r = e / GI, c = e - r * GI;
-        double acc = s_in[r + 12][c] * kGauss[0];
-        for (int j = 12; j >= 1; --j) acc = acc + (s_in[r + 12 - j][c] + s_in[r + 12 + j][c]) * kGauss[j];
-        s_v[r][c] = acc;
+        double acc = t.in[r + 12][c] * kGauss[0];
+        for (int j = 12; j >= 1; --j) acc = acc + (t.in[r + 12 - j][c] + t.in[r + 12 + j][c]) * kGauss[j];
+        t.v[r][c] = acc;
     }
     __syncthreads();
-    // axis 1: s_g[r][c] = column x0-1+c, s_v column index c+12
+    // axis 1: g[r][c] = column x0-1+c, v column index c+12
     for (int e = tid; e < GR * GR; e += 256) {
         const int r = e / GR, c = e - r * GR;
-        double acc = s_v[r][c + 12] * kGauss[0];
-        for (int j = 12; j >= 1; --j) acc = acc + (s_v[r][c + 12 - j] + s_v[r][c + 12 + j]) * kGauss[j];
-        s_g[r][c] = acc;
+        double acc = t.v[r][c + 12] * kGauss[0];
+        for (int j = 12; j >= 1; --j) acc = acc + (t.v[r][c + 12 - j] + t.v[r][c + 12 + j]) * kGauss[j];
+        t.g[r][c] = acc;
     }
     __syncthreads();
-    for (int e = tid; e < GT * GT; e += 256) {
+}
+
+// avg: [N*P][H][W] float64; one workgroup per GT x GT tile of one part of one frame.
+__global__ __launch_bounds__(256) void gauss_nms(const double* __restrict__ avg, int P, int H, int W, double thre,
+                                                 int cap, int* __restrict__ cnt, int* __restrict__ list) {
+    __shared__ GaussTile t;
+    const int x0 = blockIdx.x * GT, y0 = blockIdx.y * GT;
+    const int np = blockIdx.z;
+    gauss_tile(avg + (size_t)np * H * W, H, W, x0, y0, t);
+    for (int e = threadIdx.x; e < GT * GT; e += 256) {
         const int r = e / GT, c = e - r * GT;
         const int y = y0 + r, x = x0 + c;
         if (y >= H || x >= W) continue;
-        const double v = s_g[r + 1][c + 1];
-        const double up = y > 0 ? s_g[r][c + 1] : 0.0;
-        const double dn = y < H - 1 ? s_g[r + 2][c + 1] : 0.0;
-        const double lf = x > 0 ? s_g[r + 1][c] : 0.0;
-        const double rt = x < W - 1 ? s_g[r + 1][c + 2] : 0.0;
+        const double v = t.g[r + 1][c + 1];
+        const double up = y > 0 ? t.g[r][c + 1] : 0.0;
+        const double dn = y < H - 1 ? t.g[r + 2][c + 1] : 0.0;
+        const double lf = x > 0 ? t.g[r + 1][c] : 0.0;
+        const double rt = x < W - 1 ? t.g[r + 1][c + 2] : 0.0;
         if (v >= up && v >= dn && v >= lf && v >= rt && v > thre) {
             const int slot = atomicAdd(cnt + np, 1);
             if (slot < cap) list[(size_t)np * cap + slot] = y * W + x;
         }
     }
+}
+
+// Hand: binary = gaussian_filter(map) > thre (src/hand.py:62-63) as union-find seeds:
+// lab[i] = i where set, -1 elsewhere; cnt[np] += #set.
+__global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict__ avg, int H, int W, double thre,
+                                                       int* __restrict__ lab, int* __restrict__ cnt) {
+    __shared__ GaussTile t;
+    __shared__ int s_n;
+    const int x0 = blockIdx.x * GT, y0 = blockIdx.y * GT;
+    const int np = blockIdx.z;
+    if (threadIdx.x == 0) s_n = 0;
+    gauss_tile(avg + (size_t)np * H * W, H, W, x0, y0, t);
+    int mine = 0;
+    for (int e = threadIdx.x; e < GT * GT; e += 256) {
+        const int r = e / GT, c = e - r * GT;
+        const int y = y0 + r, x = x0 + c;
+        if (y >= H || x >= W) continue;
+        const bool on = t.g[r + 1][c + 1] > thre;
+        const int i = y * W + x;
+        lab[(size_t)np * H * W + i] = on ? i : -1;
+        mine += on;
+    }
+    if (mine) atomicAdd(&s_n, mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_n) atomicAdd(cnt + np, s_n);
 }
 
 // One workgroup per frame: order each part's peaks row-major (np.nonzero), assign the
@@ -384,6 +417,11 @@ void launch_gauss_nms(const double* avg, int NP, int H, int W, double thre, int 
                       hipStream_t st) {
     dim3 grid((W + GT - 1) / GT, (H + GT - 1) / GT, NP);
     hipLaunchKernelGGL(gauss_nms, grid, dim3(256), 0, st, avg, 18, H, W, thre, cap, cnt, list);
+}
+
+void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st) {
+    dim3 grid((W + GT - 1) / GT, (H + GT - 1) / GT, NP);
+    hipLaunchKernelGGL(gauss_threshold, grid, dim3(256), 0, st, avg, H, W, thre, lab, cnt);
 }
 
 void launch_peaks_finalize(const int* cnt, const int* list, const double* avg, int N, int H, int W,

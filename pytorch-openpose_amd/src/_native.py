@@ -47,8 +47,8 @@ def _load():
         "opose_hand_forward": (I, [P, P, I, I, I, P, I]),
         "opose_body_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, I]),
         "opose_body_post": (I, [P, P, I, I, I, I, I, I, I, C.POINTER(Params), P, I]),
-        "opose_hand_infer": (I, [P, P, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, P, I]),
-        "opose_hand_post": (I, [P, C.POINTER(P), P, P, P, P, I, I, I, C.POINTER(Params), P, P, I]),
+        "opose_hand_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, P, I]),
+        "opose_hand_post": (I, [P, C.POINTER(P), P, P, P, P, I, I, I, I, C.POINTER(Params), P, P, I]),
         "opose_profile_enable": (I, [P, I]),
         "opose_profile_reset": (I, [P]),
         "opose_profile_read": (I, [P, C.c_char_p, S]),

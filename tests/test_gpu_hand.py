@@ -1,0 +1,63 @@
+"""GPU parity for Hand(): planted 4-scale heat maps (reference fixtures, bit-exact) and an
+end-to-end seeded-network run against the oracle (keypoints equal, scores within fp32 noise)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+SCALES = (0.5, 1.0, 1.5, 2.0)
+
+
+@pytest.fixture(scope="module")
+def hand():
+    from src.hand import Hand
+    from src.weights import seeded_state_dict
+    return Hand(seeded_state_dict("hand", 0))
+
+
+def _pads(S):
+    out = []
+    for s in SCALES:
+        m = s * 368 / S
+        hs = round(S * m)
+        out.append([0, 0, (8 - hs % 8) % 8, (8 - hs % 8) % 8])
+    return out
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "hand_planted_*.npz"))), ids=os.path.basename)
+def test_hand_post_matches_reference_exactly(hand, path):
+    d = np.load(path)
+    S = int(d["size"])
+    maps = [d[f"heat{i}"][None] for i in range(4)]
+    peaks = hand.post(maps, _pads(S), S, S)[0]
+    assert peaks.dtype == d["peaks"].dtype
+    assert np.array_equal(peaks, d["peaks"])
+
+
+def test_hand_end_to_end_vs_oracle(hand):
+    from oracle import hand_post, network
+    sd = network.seeded_state_dict("hand", 0)
+    img = np.random.default_rng(3).integers(0, 256, (64, 64, 3), dtype=np.uint8)
+    ref = hand_post.hand_infer(img, lambda x: network.hand_forward(torch.from_numpy(x), sd).numpy())
+    out = hand(img)
+    assert out.shape == (21, 3) and out.dtype == ref.dtype
+    assert np.array_equal(out[:, :2], ref[:, :2])
+    np.testing.assert_allclose(out[:, 2], ref[:, 2], rtol=1e-3, atol=1e-4)
+
+
+def test_hand_batch_and_all_missing(hand):
+    # a flat grey crop: whatever the seeded network says, batch == single
+    crops = np.random.default_rng(4).integers(0, 256, (3, 48, 48, 3), dtype=np.uint8)
+    batch = hand.batch(crops)
+    for c, b in zip(crops, batch):
+        np.testing.assert_allclose(hand(c), b, rtol=1e-4, atol=1e-5)
+    # all-missing -> int64 zeros like np.array([[0, 0, 0]] * 21)
+    from src.hand import _as_reference_array
+    z = _as_reference_array(np.zeros((21, 3)), np.zeros(21, np.int32))
+    assert z.dtype == np.int64 and not z.any()
