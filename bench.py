@@ -48,6 +48,20 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic():
+    """HBM bytes per 7x7-conv launch from the committed rocprofv3 PMC summary (separate
+    --pmc passes of this same bench; scripts/gpu_profile.sh + scripts/pmc_summary.py)."""
+    path = os.path.join(REPO, "profiles", "pmc_summary.json")
+    try:
+        rec = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    for name, v in rec.items():
+        if "conv_igemm_f32<128, 128, true, 7>" in name and "hbm_bytes_per_launch" in v:
+            return v["hbm_bytes_per_launch"]
+    return None
+
+
 def cpu_baseline(frames_np, seconds):
     """Oracle (test infrastructure, used only as the timed CPU baseline) on whole frames."""
     from oracle import body_post, network
@@ -180,7 +194,8 @@ def main():
                          "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP32_TFLOPS,
                          "per_launch_flops": c7["flops"] / max(1, c7["count"]),
-                         "mean_launch_ms": c7["ms"] / max(1, c7["count"]), "traffic": None},
+                         "mean_launch_ms": c7["ms"] / max(1, c7["count"]), "traffic": pmc_traffic(),
+                         "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE)*1KiB, profiles/pmc_summary.json"},
             "network_tflops": net_flops / (net_ms * 1e-3) / 1e12 if net_ms > 0 else 0.0,
             "stage_ms_per_step": stage_ms,
             "latency_ms_single_frame": (float(np.median(lat)) * 1e3) if lat else None,

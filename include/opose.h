@@ -140,6 +140,10 @@ int opose_profile_read(opose_t* h, char* buf, size_t len);
  * mt/pt/splits <= 0 select the production tile heuristic */
 int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b, int N, int Cin, int H, int W,
                      int Cout, int ks, int pad, int relu, int mt, int pt, int splits, float* out);
+/* mean time (ms) of one conv launch (ngroups GEMM groups) on hashed data over `reps`
+ * launches; ablate bit 1 skips the im2col gather, bit 2 the weight load (timing only) */
+int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, int ks, int ngroups,
+                          int mt, int pt, int splits, int ablate, int reps, float* ms);
 /* src/body.py:38-41 for one frame and one scale: out [3,Hp,Wp]; HpWp receives (Hp, Wp)
  * (out may be NULL to query the size) */
 int opose_debug_preprocess(opose_t* h, const uint8_t* bgr, int H, int W, double scale, int pad_value,

@@ -46,6 +46,7 @@ struct ConvArgs {
     int splits;         // split-K factor (gridDim.z = ngroups * splits)
     int chunks_per_split;
     float* partial;     // [ngroups][splits][Mpad][npix] when splits > 1
+    int ablate;         // timing-only ablations (opose_debug_conv_time): 1 no B gather, 2 no A load
 };
 
 // ---------------------------------------------------------------- body records

@@ -36,8 +36,10 @@ constexpr int NT = 256;  // threads per workgroup
 // TAP: K ordered (tap, channel) with Cin padded to a multiple of KC -> one bounds check per
 // pixel per chunk and a wave-uniform channel stride (all layers with Cin >= 32); otherwise K is
 // the OIHW flattening decoded through `ktab` (conv1_1: K = 27).
-template <int MT, int PT, bool TAP>
+// KS: compile-time kernel size (1, 3, 7) so the tap decode folds; 0 = runtime a.ks.
+template <int MT, int PT, bool TAP, int KS>
 __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* __restrict__ ktab) {
+    const int ks = KS ? KS : a.ks;
     constexpr int WM = MT / 2, WP = PT / 2;
     constexpr int TM = WM / 32, TN = WP / 32;
     constexpr int PJ = PT / 64;             // pixel columns per lane
@@ -54,13 +56,25 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l31 = lane & 31, hk = lane >> 5;
 
-    const int zg = blockIdx.z;
+    // XCD-aware tile order (guide T1, bijective form): the dispatcher deals workgroups
+    // round-robin over the 8 XCDs, so give XCD x a contiguous run of tiles instead — the
+    // M-tiles of one pixel tile and neighbouring pixel tiles (which share im2col halo rows)
+    // then share that XCD's L2.  Speed only: any placement is correct.
+    const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
+    const int total = gridDim.x;
+    const int b = blockIdx.x;
+    const int q = total >> 3, rr = total & 7, xcd = b & 7;
+    const int id = xcd * q + min(xcd, rr) + (b >> 3);
+    const int mt = id % nM;
+    const int rest = id / nM;
+    const int pt = rest % nP;
+    const int zg = rest / nP;
     const int g = zg / a.splits;
     const int split = zg - g * a.splits;
     const ConvGroup G = g == 0 ? a.g[0] : a.g[1];  // no dynamic kernarg indexing
 
-    const int p0 = blockIdx.x * PT;
-    const int m0 = blockIdx.y * MT;
+    const int p0 = pt * PT;
+    const int m0 = mt * MT;
     const int HW = a.H * a.W;
     float* s_bias = lds + 2 * (A_SZ + B_SZ);
     if (tid < MT) s_bias[tid] = (m0 + tid < G.cout) ? G.bias[m0 + tid] : 0.f;
@@ -104,11 +118,11 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
 
     auto chunk_setup = [&](int c) __attribute__((always_inline)) {
         if constexpr (TAP) {
-            const int cpt = a.Kpad / (KC * a.ks * a.ks);  // chunks per tap (wave-uniform scalars)
+            const int cpt = a.Kpad / (KC * ks * ks);  // chunks per tap (wave-uniform scalars)
             const int tap = c / cpt;
             ch0 = (c - tap * cpt) * KC + wave * RW;
-            const int ky = tap / a.ks;
-            const int dy = ky - a.pad, dx = tap - ky * a.ks - a.pad;
+            const int ky = tap / ks;
+            const int dy = ky - a.pad, dx = tap - ky * ks - a.pad;
             const int shift = dy * a.W + dx;
 #pragma unroll
             for (int j = 0; j < PJ; ++j) {
@@ -121,6 +135,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
     };
     // issue the LDS-DMA of B row r (this wave's) of chunk c into stage `buf`
     auto dma_b_row = [&](int c, int buf, int r) __attribute__((always_inline)) {
+        if (a.ablate & 1) return;
         float* Bs = lds + buf * (A_SZ + B_SZ) + A_SZ + (wave * RW + r) * PT;
         if constexpr (TAP) {
             const int ch = min(ch0 + r, a.Cin - 1);  // padded channels: any valid address (weights are 0)
@@ -144,6 +159,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
         }
     };
     auto dma_a = [&](int c, int buf) __attribute__((always_inline)) {
+        if (a.ablate & 2) return;
         const int k0 = c * KC;
         float* As = lds + buf * (A_SZ + B_SZ);
 #pragma unroll
@@ -242,6 +258,21 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
     }
 }
 
+// fills a buffer with a cheap hash in [-1, 1) (timing runs must not run on zeros: DVFS)
+__global__ void fill_hash(float* p, size_t n, uint32_t seed) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+        h ^= h >> 15;
+        h *= 2246822519u;
+        h ^= h >> 13;
+        p[i] = (float)(h & 0xffffff) / 8388608.f - 1.f;
+    }
+}
+
+void launch_fill_hash(float* p, size_t n, uint32_t seed, hipStream_t st) {
+    hipLaunchKernelGGL(fill_hash, dim3(2048), dim3(256), 0, st, p, n, seed);
+}
+
 // Deterministic split-K combine: slabs summed in split order, then bias + ReLU.
 __global__ __launch_bounds__(256) void conv_splitk_reduce(ConvArgs a) {
     const int g = blockIdx.y;
@@ -281,11 +312,17 @@ __global__ __launch_bounds__(256) void maxpool2x2(const float* __restrict__ in, 
 // ------------------------------------------------------------------ host launchers
 template <int MT, int PT>
 static void launch_tile(const ConvArgs& a, int ngroups, const int* ktab, hipStream_t st) {
-    dim3 grid((a.npix + PT - 1) / PT, a.Mpad / MT, ngroups * a.splits);
-    if (a.tap_major)
-        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true>), grid, dim3(NT), 0, st, a, ktab);
+    dim3 grid(((a.npix + PT - 1) / PT) * (a.Mpad / MT) * ngroups * a.splits);
+    if (!a.tap_major)
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, false, 0>), grid, dim3(NT), 0, st, a, ktab);
+    else if (a.ks == 7)
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 7>), grid, dim3(NT), 0, st, a, ktab);
+    else if (a.ks == 3)
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 3>), grid, dim3(NT), 0, st, a, ktab);
+    else if (a.ks == 1)
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 1>), grid, dim3(NT), 0, st, a, ktab);
     else
-        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, false>), grid, dim3(NT), 0, st, a, ktab);
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 0>), grid, dim3(NT), 0, st, a, ktab);
 }
 
 void launch_conv(const ConvArgs& a, int ngroups, const int* ktab, int mt, int pt, hipStream_t st) {

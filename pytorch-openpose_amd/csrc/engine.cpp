@@ -971,6 +971,57 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
     return OPOSE_OK;
 }
 
+// timing of one conv launch configuration on hashed data (ablate: see ConvArgs::ablate)
+int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, int ks, int ngroups, int mt, int pt,
+                          int splits, int ablate, int reps, float* ms) {
+    if (!h || !ms || reps < 1 || ngroups < 1 || ngroups > 2) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        Spec s{"timing", Cin, Cout, ks, ks / 2};
+        std::vector<float> w((size_t)Cout * Cin * ks * ks, 0.01f), b(Cout, 0.f);
+        upload_conv(h, 0, "__timing__", {&s}, {w.data()}, {b.data()});
+        DevConv* c = h->convs[0]["__timing__"].get();
+        launch_fill_hash(c->wt, (size_t)c->Kpad * c->Mpad, 7, h->stream);
+        DevBuf xin, yout;
+        const size_t nx = (size_t)ngroups * N * Cin * H * W, ny = (size_t)ngroups * N * Cout * H * W;
+        float* xd = xin.ensure<float>(nx, h->stream);
+        float* yd = yout.ensure<float>(ny, h->stream);
+        launch_fill_hash(xd, nx, 3, h->stream);
+        ConvArgs a{};
+        a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.ks = ks; a.pad = ks / 2;
+        a.K = c->K; a.Kpad = c->Kpad; a.Mpad = c->Mpad; a.npix = N * H * W;
+        a.tap_major = c->tap_major ? 1 : 0;
+        a.ablate = ablate;
+        for (int g = 0; g < 2; ++g) {
+            ConvGroup& G = a.g[g];
+            const int gg = g < ngroups ? g : 0;
+            G.in = xd + (size_t)gg * N * Cin * H * W; G.in_cstride = Cin; G.in_coff = 0; G.wt = c->wt; G.bias = c->bias;
+            G.out = yd + (size_t)gg * N * Cout * H * W; G.out_cstride = Cout; G.out_coff = 0; G.out2 = nullptr;
+            G.cout = Cout; G.relu = 1;
+        }
+        TileChoice t = choose_tile(a.Mpad, a.npix, ngroups, a.Kpad / 32);
+        if (mt > 0) { t.mt = mt; t.pt = pt; }
+        if (splits > 0) { t.splits = splits; t.cps = (a.Kpad / 32 + splits - 1) / splits; }
+        if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
+        a.splits = t.splits; a.chunks_per_split = t.cps;
+        if (t.splits > 1) a.partial = h->partial.ensure<float>((size_t)ngroups * t.splits * a.Mpad * a.npix, h->stream);
+        launch_conv(a, ngroups, c->ktab, t.mt, t.pt, h->stream);  // warm-up
+        hipEvent_t e0, e1;
+        OPOSE_HIP_CHECK(hipEventCreate(&e0));
+        OPOSE_HIP_CHECK(hipEventCreate(&e1));
+        OPOSE_HIP_CHECK(hipEventRecord(e0, h->stream));
+        for (int r = 0; r < reps; ++r) launch_conv(a, ngroups, c->ktab, t.mt, t.pt, h->stream);
+        OPOSE_HIP_CHECK(hipEventRecord(e1, h->stream));
+        OPOSE_HIP_CHECK(hipEventSynchronize(e1));
+        OPOSE_HIP_CHECK(hipEventElapsedTime(ms, e0, e1));
+        *ms /= reps;
+        OPOSE_HIP_CHECK(hipEventDestroy(e0));
+        OPOSE_HIP_CHECK(hipEventDestroy(e1));
+        h->convs[0].erase("__timing__");
+    });
+    return OPOSE_OK;
+}
+
 int opose_debug_preprocess(opose_t* h, const uint8_t* bgr, int H, int W, double scale, int pad_value, float* out,
                            int* HpWp) {
     if (!h || !bgr || !HpWp) return OPOSE_E_ARG;

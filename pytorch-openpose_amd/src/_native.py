@@ -54,6 +54,7 @@ def _load():
         "opose_profile_read": (I, [P, C.c_char_p, S]),
         "opose_debug_conv": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P]),
         "opose_debug_preprocess": (I, [P, P, I, I, D, I, P, P]),
+        "opose_debug_conv_time": (I, [P, I, I, I, I, I, I, I, I, I, I, I, I, P]),
         "opose_debug_heat": (I, [P, P, I, I, I, I, I, I, P, P]),
     }
     for name, (res, args) in sig.items():
@@ -70,7 +71,7 @@ EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last
             "opose_get_stream", "opose_synchronize", "opose_set_capacity", "opose_body_record_bytes",
             "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_body_infer",
             "opose_body_post", "opose_hand_infer", "opose_hand_post", "opose_profile_enable",
-            "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_preprocess",
+            "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_conv_time", "opose_debug_preprocess",
             "opose_debug_heat"]
 
 

@@ -21,4 +21,5 @@ run pmc2 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_
 run pmc3 --pmc FETCH_SIZE
 run pmc4 --pmc WRITE_SIZE
 run pmc5 --pmc TCC_HIT_sum TCC_MISS_sum SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
+python3 scripts/pmc_summary.py $OUT --json $OUT/pmc_summary.json --top 12 > $OUT/pmc_summary.txt 2>&1
 exit 0
