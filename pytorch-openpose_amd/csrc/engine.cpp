@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -155,10 +156,11 @@ struct opose_ctx {
     bool loaded[2] = {false, false};
     // workspace
     DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[kMaxScales], avg, cnt, list, peak_pos, part_cnt,
-        score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound;
+        score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score;
     // profiling
     bool prof = false;
     bool detail = false;  // per-layer aggregation (opose_profile_enable(h, 2))
+    bool fused_heat = getenv("OPOSE_FUSED_HEAT") != nullptr;  // A/B switch for the heat chain
     std::vector<ProfEntry> pending;
     std::map<std::string, ProfAgg> agg;
     std::vector<hipEvent_t> event_pool;
@@ -513,28 +515,6 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     const RecordLayout L = make_record_layout(h->ppp, h->maxp);
     const int cap = h->ppp;
     const int ns = (int)gs.size();
-    double* avg = h->avg.ensure<double>((size_t)N * 18 * H * W, h->stream);
-    ProfEntry pe;
-    for (int s = 0; s < ns; ++s) {
-        h->prof_begin(pe, "heat_full", 0, (double)N * 18 * H * W * 8 * (s ? 2 : 1));
-        launch_heat_full(h->mids[s].ensure<float>(0, h->stream), 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W,
-                         gs[s].up_sy, gs[s].up_sx, ns, s > 0, avg, h->stream);
-        h->prof_end(pe);
-    }
-    int* cnt = h->cnt.ensure<int>((size_t)N * 18, h->stream);
-    int* list = h->list.ensure<int>((size_t)N * 18 * cap, h->stream);
-    int* pos = h->peak_pos.ensure<int>((size_t)N * 18 * cap, h->stream);
-    int* pcnt = h->part_cnt.ensure<int>((size_t)N * 18, h->stream);
-    double* score = h->score.ensure<double>((size_t)N * 19 * cap * cap, h->stream);
-    Conn* conn = h->conn.ensure<Conn>((size_t)N * 19 * cap, h->stream);
-    int* ccnt = h->conn_cnt.ensure<int>((size_t)N * 19, h->stream);
-    OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * N * 18, h->stream));
-    h->prof_begin(pe, "gauss_nms", 0, (double)N * 18 * H * W * 8);
-    launch_gauss_nms(avg, N * 18, H, W, p.thre1, cap, cnt, list, h->stream);
-    h->prof_end(pe);
-    h->prof_begin(pe, "peaks_finalize", 0, 0);
-    launch_peaks_finalize(cnt, list, avg, N, H, W, L, rec_dev, pos, pcnt, h->stream);
-    h->prof_end(pe);
     PafScales S{};
     for (int s = 0; s < ns; ++s) {
         S.mid[s] = h->mids[s].ensure<float>(0, h->stream);
@@ -547,6 +527,36 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     S.cm = 56;
     S.H = H;
     S.W = W;
+    int* cnt = h->cnt.ensure<int>((size_t)N * 18, h->stream);
+    int* list = h->list.ensure<int>((size_t)N * 18 * cap, h->stream);
+    double* lscore = h->list_score.ensure<double>((size_t)N * 18 * cap, h->stream);
+    int* pos = h->peak_pos.ensure<int>((size_t)N * 18 * cap, h->stream);
+    int* pcnt = h->part_cnt.ensure<int>((size_t)N * 18, h->stream);
+    double* score = h->score.ensure<double>((size_t)N * 19 * cap * cap, h->stream);
+    Conn* conn = h->conn.ensure<Conn>((size_t)N * 19 * cap, h->stream);
+    int* ccnt = h->conn_cnt.ensure<int>((size_t)N * 19, h->stream);
+    OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * N * 18, h->stream));
+    ProfEntry pe;
+    if (h->fused_heat) {
+        // heat average (src/body.py:55-67) evaluated on the fly inside the Gaussian tiles
+        h->prof_begin(pe, "gauss_nms", 0, (double)N * 18 * 4.0 * gs[0].Hs * gs[0].Ws * ns);
+        launch_gauss_nms_fused(S, N, 38, p.thre1, cap, cnt, list, lscore, h->stream);
+        h->prof_end(pe);
+    } else {
+        double* avg = h->avg.ensure<double>((size_t)N * 18 * H * W, h->stream);
+        for (int s = 0; s < ns; ++s) {
+            h->prof_begin(pe, "heat_full", 0, (double)N * 18 * H * W * 8 * (s ? 2 : 1));
+            launch_heat_full(S.mid[s], 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx, ns, s > 0,
+                             avg, h->stream);
+            h->prof_end(pe);
+        }
+        h->prof_begin(pe, "gauss_nms", 0, (double)N * 18 * H * W * 8);
+        launch_gauss_nms(avg, N * 18, H, W, p.thre1, cap, cnt, list, lscore, h->stream);
+        h->prof_end(pe);
+    }
+    h->prof_begin(pe, "peaks_finalize", 0, 0);
+    launch_peaks_finalize(cnt, list, lscore, N, H, W, L, rec_dev, pos, pcnt, h->stream);
+    h->prof_end(pe);
     h->prof_begin(pe, "paf_score", 0, 0);
     launch_paf_score(S, pos, pcnt, N, cap, p.thre2, score, h->stream);
     h->prof_end(pe);

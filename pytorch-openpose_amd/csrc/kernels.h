@@ -34,9 +34,11 @@ void launch_heat_full(const float* mid, int Cm, int coff, int P, int N, int Hs, 
 
 // post.hip
 void launch_gauss_nms(const double* avg, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
-                      hipStream_t st);
+                      double* list_score, hipStream_t st);
+void launch_gauss_nms_fused(const PafScales& S, int N, int ch0, double thre, int cap, int* cnt, int* list,
+                            double* list_score, hipStream_t st);
 void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st);
-void launch_peaks_finalize(const int* cnt, const int* list, const double* avg, int N, int H, int W,
+void launch_peaks_finalize(const int* cnt, const int* list, const double* list_score, int N, int H, int W,
                            const RecordLayout& L, uint8_t* records, int* peak_pos, int* part_cnt, hipStream_t st);
 void launch_paf_score(const PafScales& S, const int* peak_pos, const int* part_cnt, int N, int cap, double thre2,
                       double* score, hipStream_t st);

@@ -48,35 +48,69 @@ struct GaussTile {
     double g[GR][GR];
 };
 
-__device__ __forceinline__ void gauss_tile(const double* __restrict__ m, int H, int W, int x0, int y0, GaussTile& t) {
+constexpr int FR_V = 9;   // rows per thread in the vertical pass   (34 <= 4 x 9)
+constexpr int FR_H = 5;   // cols per thread in the horizontal pass (34 <= 7 x 5)
+
+// The two 25-tap passes over a loaded tile, each thread sliding a register window along a
+// column (axis 0) or row (axis 1): one LDS read per output instead of 25.
+__device__ __forceinline__ void gauss_passes(GaussTile& t) {
     const int tid = threadIdx.x;
-    for (int e = tid; e < GI * GI; e += 256) {
-        const int r = e / GI, c = e - r * GI;
-        const int gy = reflect_idx(y0 - 13 + r, H), gx = reflect_idx(x0 - 13 + c, W);
-        t.in[r][c] = m[(size_t)gy * W + gx];
+    if (tid < 4 * GI) {  // axis 0: thread -> (column c, 9-row run)
+        const int c = tid % GI, r0 = (tid / GI) * FR_V;
+        double win[FR_V + 24];
+#pragma unroll
+        for (int i = 0; i < FR_V + 24; ++i) win[i] = (r0 + i < GI) ? t.in[r0 + i][c] : 0.0;
+#pragma unroll
+        for (int i = 0; i < FR_V; ++i) {
+            if (r0 + i < GR) {
+                double acc = win[i + 12] * kGauss[0];
+#pragma unroll
+                for (int j = 12; j >= 1; --j) acc = acc + (win[i + 12 - j] + win[i + 12 + j]) * kGauss[j];
+                t.v[r0 + i][c] = acc;
+            }
+        }
     }
     __syncthreads();
-    // axis 0 (scipy's first pass): v[r][c] = rows y0-1+r, input row index r+12
-    for (int e = tid; e < GR * GI; e += 256) {
-        const int r = e / GI, c = e - r * GI;
-        double acc = t.in[r + 12][c] * kGauss[0];
-        for (int j = 12; j >= 1; --j) acc = acc + (t.in[r + 12 - j][c] + t.in[r + 12 + j][c]) * kGauss[j];
-        t.v[r][c] = acc;
-    }
-    __syncthreads();
-    // axis 1: g[r][c] = column x0-1+c, v column index c+12
-    for (int e = tid; e < GR * GR; e += 256) {
-        const int r = e / GR, c = e - r * GR;
-        double acc = t.v[r][c + 12] * kGauss[0];
-        for (int j = 12; j >= 1; --j) acc = acc + (t.v[r][c + 12 - j] + t.v[r][c + 12 + j]) * kGauss[j];
-        t.g[r][c] = acc;
+    if (tid < 7 * GR) {  // axis 1: thread -> (row r, 5-column run)
+        const int r = tid % GR, c0 = (tid / GR) * FR_H;
+        double win[FR_H + 24];
+#pragma unroll
+        for (int i = 0; i < FR_H + 24; ++i) win[i] = (c0 + i < GI) ? t.v[r][c0 + i] : 0.0;
+#pragma unroll
+        for (int i = 0; i < FR_H; ++i) {
+            if (c0 + i < GR) {
+                double acc = win[i + 12] * kGauss[0];
+#pragma unroll
+                for (int j = 12; j >= 1; --j) acc = acc + (win[i + 12 - j] + win[i + 12 + j]) * kGauss[j];
+                t.g[r][c0 + i] = acc;
+            }
+        }
     }
     __syncthreads();
 }
 
+__device__ __forceinline__ void gauss_tile(const double* __restrict__ m, int H, int W, int x0, int y0, GaussTile& t) {
+    constexpr int IIT = (GI * GI + 255) / 256;
+    double iv[IIT];
+#pragma unroll
+    for (int it = 0; it < IIT; ++it) {  // all loads of a thread in flight together
+        const int e = min((int)threadIdx.x + it * 256, GI * GI - 1);
+        const int r = e / GI, c = e - r * GI;
+        iv[it] = m[(size_t)reflect_idx(y0 - 13 + r, H) * W + reflect_idx(x0 - 13 + c, W)];
+    }
+#pragma unroll
+    for (int it = 0; it < IIT; ++it) {
+        const int e = threadIdx.x + it * 256;
+        if (e < GI * GI) t.in[e / GI][e % GI] = iv[it];
+    }
+    __syncthreads();
+    gauss_passes(t);
+}
+
 // avg: [N*P][H][W] float64; one workgroup per GT x GT tile of one part of one frame.
 __global__ __launch_bounds__(256) void gauss_nms(const double* __restrict__ avg, int P, int H, int W, double thre,
-                                                 int cap, int* __restrict__ cnt, int* __restrict__ list) {
+                                                 int cap, int* __restrict__ cnt, int* __restrict__ list,
+                                                 double* __restrict__ list_score) {
     __shared__ GaussTile t;
     const int x0 = blockIdx.x * GT, y0 = blockIdx.y * GT;
     const int np = blockIdx.z;
@@ -92,7 +126,155 @@ __global__ __launch_bounds__(256) void gauss_nms(const double* __restrict__ avg,
         const double rt = x < W - 1 ? t.g[r + 1][c + 2] : 0.0;
         if (v >= up && v >= dn && v >= lf && v >= rt && v > thre) {
             const int slot = atomicAdd(cnt + np, 1);
-            if (slot < cap) list[(size_t)np * cap + slot] = y * W + x;
+            if (slot < cap) {
+                list[(size_t)np * cap + slot] = y * W + x;
+                list_score[(size_t)np * cap + slot] = t.in[r + 13][c + 13];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused body heat chain: the scale-averaged full-resolution heat value
+//   heat_avg[y, x] = sum_s (double)(resize_s(x8 map_s)[y, x] / n_scales)     (src/body.py:55-67)
+// is evaluated on the fly from the x8 maps while the Gaussian tile is loaded, so the 18 float64
+// full-resolution maps are never written or re-read.  The 25-tap passes use per-thread
+// register windows (one LDS read per output instead of 25); the arithmetic order is scipy's.
+__device__ __forceinline__ double heat_avg_at(const PafScales& S, int n, int ch, int Y, int X) {
+    double acc = 0.0;
+    for (int s = 0; s < S.n; ++s) {
+        const float* plane = S.mid[s] + ((size_t)n * S.cm + ch) * S.hs[s] * S.ws[s];
+        float v;
+        if (S.hs[s] == S.H && S.ws[s] == S.W) {
+            v = plane[(size_t)Y * S.ws[s] + X];
+        } else {
+            const CubicTap ty = cubic_tap(Y, S.sy[s], S.hs[s]);
+            const CubicTap tx = cubic_tap(X, S.sx[s], S.ws[s]);
+            v = cubic_sample_f32(plane, S.ws[s], ty, tx);
+        }
+        v = v / (float)S.n;
+        acc = acc + (double)v;
+    }
+    return acc;
+}
+
+__global__ __launch_bounds__(256) void gauss_nms_fused(PafScales S, int ch0, double thre, int cap,
+                                                       int* __restrict__ cnt, int* __restrict__ list,
+                                                       double* __restrict__ list_score) {
+    __shared__ GaussTile t;
+    __shared__ CubicTap s_ty[GI], s_tx[GI];  // per-tile resize taps of the (reflected) rows / cols
+    __shared__ int s_rlo, s_rhi;
+    constexpr int HB_ROWS = (GR * GI) / GI;   // horizontal-pass rows that fit in t.v (34)
+    float* hbuf = reinterpret_cast<float*>(&t.v[0][0]);  // [src row][tile col], reuses t.v
+    constexpr int HB_CAP = (int)(sizeof(t.v) / sizeof(float)) / GI;
+    (void)HB_ROWS;
+    const int tid = threadIdx.x;
+    const int x0 = blockIdx.x * GT, y0 = blockIdx.y * GT;
+    const int np = blockIdx.z;
+    const int n = np / 18, part = np - n * 18;
+    const int H = S.H, W = S.W;
+    for (int s = 0; s < S.n; ++s) {
+        const bool ident = S.hs[s] == S.H && S.ws[s] == S.W;
+        const float* plane = S.mid[s] + ((size_t)n * S.cm + ch0 + part) * S.hs[s] * S.ws[s];
+        if (ident) {
+            constexpr int IIT = (GI * GI + 255) / 256;
+            float iv[IIT];
+#pragma unroll
+            for (int it = 0; it < IIT; ++it) {
+                const int e = min(tid + it * 256, GI * GI - 1);
+                const int r = e / GI, c = e - r * GI;
+                iv[it] = plane[(size_t)reflect_idx(y0 - 13 + r, H) * S.ws[s] + reflect_idx(x0 - 13 + c, W)];
+            }
+#pragma unroll
+            for (int it = 0; it < IIT; ++it) {
+                const int e = tid + it * 256;
+                if (e < GI * GI) {
+                    const int r = e / GI, c = e - r * GI;
+                    const float v = iv[it] / (float)S.n;
+                    t.in[r][c] = (s == 0 ? 0.0 : t.in[r][c]) + (double)v;
+                }
+            }
+            __syncthreads();
+            continue;
+        }
+        if (tid < GI) s_ty[tid] = cubic_tap(reflect_idx(y0 - 13 + tid, H), S.sy[s], S.hs[s]);
+        else if (tid < 2 * GI) s_tx[tid - GI] = cubic_tap(reflect_idx(x0 - 13 + tid - GI, W), S.sx[s], S.ws[s]);
+        if (tid == 0) {
+            s_rlo = 0x7fffffff;
+            s_rhi = -1;
+        }
+        __syncthreads();
+        if (tid < GI) {
+            atomicMin(&s_rlo, s_ty[tid].i[0]);
+            atomicMax(&s_rhi, s_ty[tid].i[3]);
+        }
+        __syncthreads();
+        const int rlo = s_rlo, nrows = s_rhi - s_rlo + 1;
+        if (nrows <= HB_CAP) {
+            // OpenCV's separable order: horizontal interpolation of each needed source row once,
+            // then the vertical combination per output (identical float32 values).
+            // fixed trip count, fully unrolled: all 32 loads of a thread are in flight together
+            constexpr int HIT = (HB_CAP * GI + 255) / 256;
+            float hv[HIT][4];
+#pragma unroll
+            for (int it = 0; it < HIT; ++it) {
+                const int e = tid + it * 256;
+                const int rr = e / GI, c = e - rr * GI;
+                const bool ok = e < nrows * GI;
+                const float* row = plane + (size_t)(rlo + (ok ? rr : 0)) * S.ws[s];
+                const CubicTap& tx = s_tx[ok ? c : 0];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) hv[it][j] = row[tx.i[j]];
+            }
+#pragma unroll
+            for (int it = 0; it < HIT; ++it) {
+                const int e = tid + it * 256;
+                if (e < nrows * GI) {
+                    const CubicTap& tx = s_tx[e % GI];
+                    float v = hv[it][0] * tx.c[0];
+                    v = v + hv[it][1] * tx.c[1];
+                    v = v + hv[it][2] * tx.c[2];
+                    v = v + hv[it][3] * tx.c[3];
+                    hbuf[e] = v;
+                }
+            }
+            __syncthreads();
+            for (int e = tid; e < GI * GI; e += 256) {
+                const int r = e / GI, c = e - r * GI;
+                const CubicTap& ty = s_ty[r];
+                float v = hbuf[(ty.i[0] - rlo) * GI + c] * ty.c[0];
+                v = v + hbuf[(ty.i[1] - rlo) * GI + c] * ty.c[1];
+                v = v + hbuf[(ty.i[2] - rlo) * GI + c] * ty.c[2];
+                v = v + hbuf[(ty.i[3] - rlo) * GI + c] * ty.c[3];
+                v = v / (float)S.n;
+                t.in[r][c] = (s == 0 ? 0.0 : t.in[r][c]) + (double)v;
+            }
+        } else {  // strong downscale: direct 16-tap evaluation
+            for (int e = tid; e < GI * GI; e += 256) {
+                const int r = e / GI, c = e - r * GI;
+                float v = cubic_sample_f32(plane, S.ws[s], s_ty[r], s_tx[c]);
+                v = v / (float)S.n;
+                t.in[r][c] = (s == 0 ? 0.0 : t.in[r][c]) + (double)v;
+            }
+        }
+        __syncthreads();
+    }
+    gauss_passes(t);
+    for (int e = tid; e < GT * GT; e += 256) {
+        const int r = e / GT, c = e - r * GT;
+        const int y = y0 + r, x = x0 + c;
+        if (y >= H || x >= W) continue;
+        const double v = t.g[r + 1][c + 1];
+        const double up = y > 0 ? t.g[r][c + 1] : 0.0;
+        const double dn = y < H - 1 ? t.g[r + 2][c + 1] : 0.0;
+        const double lf = x > 0 ? t.g[r + 1][c] : 0.0;
+        const double rt = x < W - 1 ? t.g[r + 1][c + 2] : 0.0;
+        if (v >= up && v >= dn && v >= lf && v >= rt && v > thre) {
+            const int slot = atomicAdd(cnt + np, 1);
+            if (slot < cap) {
+                list[(size_t)np * cap + slot] = y * W + x;
+                list_score[(size_t)np * cap + slot] = t.in[r + 13][c + 13];  // map_ori[y, x]
+            }
         }
     }
 }
@@ -125,7 +307,7 @@ __global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict_
 // One workgroup per frame: order each part's peaks row-major (np.nonzero), assign the
 // global running ids, write candidate rows (x, y, score, id) into the record.
 __global__ __launch_bounds__(256) void peaks_finalize(const int* __restrict__ cnt, const int* __restrict__ list,
-                                                      const double* __restrict__ avg, int H, int W, RecordLayout L,
+                                                      const double* __restrict__ list_score, int H, int W, RecordLayout L,
                                                       uint8_t* __restrict__ records, int* __restrict__ peak_pos,
                                                       int* __restrict__ part_cnt) {
     const int n = blockIdx.x;
@@ -163,7 +345,7 @@ __global__ __launch_bounds__(256) void peaks_finalize(const int* __restrict__ cn
             double* row = cand + (size_t)id * 4;
             row[0] = (double)x;
             row[1] = (double)y;
-            row[2] = avg[(((size_t)n * 18 + p) * H + y) * W + x];
+            row[2] = list_score[((size_t)n * 18 + p) * cap + i];
             row[3] = (double)id;
             peak_pos[((size_t)n * 18 + p) * cap + rank] = v;
         }
@@ -414,9 +596,9 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
 
 // ------------------------------------------------------------------ launchers
 void launch_gauss_nms(const double* avg, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
-                      hipStream_t st) {
+                      double* list_score, hipStream_t st) {
     dim3 grid((W + GT - 1) / GT, (H + GT - 1) / GT, NP);
-    hipLaunchKernelGGL(gauss_nms, grid, dim3(256), 0, st, avg, 18, H, W, thre, cap, cnt, list);
+    hipLaunchKernelGGL(gauss_nms, grid, dim3(256), 0, st, avg, 18, H, W, thre, cap, cnt, list, list_score);
 }
 
 void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st) {
@@ -424,10 +606,16 @@ void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre
     hipLaunchKernelGGL(gauss_threshold, grid, dim3(256), 0, st, avg, H, W, thre, lab, cnt);
 }
 
-void launch_peaks_finalize(const int* cnt, const int* list, const double* avg, int N, int H, int W,
+void launch_peaks_finalize(const int* cnt, const int* list, const double* list_score, int N, int H, int W,
                            const RecordLayout& L, uint8_t* records, int* peak_pos, int* part_cnt, hipStream_t st) {
-    hipLaunchKernelGGL(peaks_finalize, dim3(N), dim3(256), 0, st, cnt, list, avg, H, W, L, records, peak_pos,
+    hipLaunchKernelGGL(peaks_finalize, dim3(N), dim3(256), 0, st, cnt, list, list_score, H, W, L, records, peak_pos,
                        part_cnt);
+}
+
+void launch_gauss_nms_fused(const PafScales& S, int N, int ch0, double thre, int cap, int* cnt, int* list,
+                            double* list_score, hipStream_t st) {
+    dim3 grid((S.W + GT - 1) / GT, (S.H + GT - 1) / GT, N * 18);
+    hipLaunchKernelGGL(gauss_nms_fused, grid, dim3(256), 0, st, S, ch0, thre, cap, cnt, list, list_score);
 }
 
 void launch_paf_score(const PafScales& S, const int* peak_pos, const int* part_cnt, int N, int cap, double thre2,
