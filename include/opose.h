@@ -137,7 +137,8 @@ int opose_profile_read(opose_t* h, char* buf, size_t len);
 
 /* ---- test hooks (parity tests call single stages; host pointers, synchronous) ----- */
 /* one stride-1 conv: x [N,Cin,H,W], w [Cout,Cin,ks,ks], b [Cout] -> out [N,Cout,H,W];
- * mt/pt/splits <= 0 select the production tile heuristic */
+ * mt/pt <= 0 select the production tile heuristic; splits > 0 forces that many stream-K
+ * workgroups (== number of tiles: plain data-parallel grid) */
 int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b, int N, int Cin, int H, int W,
                      int Cout, int ks, int pad, int relu, int mt, int pt, int splits, float* out);
 /* mean time (ms) of one conv launch (ngroups GEMM groups) on hashed data over `reps`

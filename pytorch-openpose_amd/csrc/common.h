@@ -43,10 +43,9 @@ struct ConvArgs {
     int K, Kpad, Mpad;  // K = Cin*ks*ks
     int npix;           // N*H*W
     int tap_major;      // K ordered (tap, channel) with Cin padded to 32 (else OIHW + ktab)
-    int splits;         // split-K factor (gridDim.z = ngroups * splits)
-    int chunks_per_split;
-    float* partial;     // [ngroups][splits][Mpad][npix] when splits > 1
-    int ablate;         // timing-only ablations (opose_debug_conv_time): 1 no B gather, 2 no A load
+    int ngroups;        // 1 or 2 GEMM groups sharing the launch
+    int sk_grid;        // stream-K workgroups (== tiles: plain data-parallel grid)
+    float* partial;     // stream-K partial slabs [2 * sk_grid][MT * PT]
 };
 
 // ---------------------------------------------------------------- body records

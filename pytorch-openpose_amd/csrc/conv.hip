@@ -37,7 +37,9 @@ constexpr int NT = 256;  // threads per workgroup
 // pixel per chunk and a wave-uniform channel stride (all layers with Cin >= 32); otherwise K is
 // the OIHW flattening decoded through `ktab` (conv1_1: K = 27).
 // KS: compile-time kernel size (1, 3, 7) so the tap decode folds; 0 = runtime a.ks.
-template <int MT, int PT, bool TAP, int KS>
+// ABL: timing-only ablations (never launched in production): 1 skip the im2col gather,
+// 2 skip the weight load, 4 skip the LDS fragment reads, 8 skip the per-chunk barrier.
+template <int MT, int PT, bool TAP, int KS, int ABL = 0>
 __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* __restrict__ ktab) {
     const int ks = KS ? KS : a.ks;
     constexpr int WM = MT / 2, WP = PT / 2;
@@ -55,127 +57,133 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l31 = lane & 31, hk = lane >> 5;
-
-    // XCD-aware tile order (guide T1, bijective form): the dispatcher deals workgroups
-    // round-robin over the 8 XCDs, so give XCD x a contiguous run of tiles instead — the
-    // M-tiles of one pixel tile and neighbouring pixel tiles (which share im2col halo rows)
-    // then share that XCD's L2.  Speed only: any placement is correct.
     const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
-    const int total = gridDim.x;
-    const int b = blockIdx.x;
-    const int q = total >> 3, rr = total & 7, xcd = b & 7;
-    const int id = xcd * q + min(xcd, rr) + (b >> 3);
-    const int mt = id % nM;
-    const int rest = id / nM;
-    const int pt = rest % nP;
-    const int zg = rest / nP;
-    const int g = zg / a.splits;
-    const int split = zg - g * a.splits;
-    const ConvGroup G = g == 0 ? a.g[0] : a.g[1];  // no dynamic kernarg indexing
-
-    const int p0 = pt * PT;
-    const int m0 = mt * MT;
+    const int nK = a.Kpad / KC;
     const int HW = a.H * a.W;
-    float* s_bias = lds + 2 * (A_SZ + B_SZ);
-    if (tid < MT) s_bias[tid] = (m0 + tid < G.cout) ? G.bias[m0 + tid] : 0.f;
-
-    // ---- per-lane pixel state for the im2col gather.  The activation is read through a
-    // buffer resource: an invalid (zero-padding) tap gets a byte offset >= num_records, which
-    // the hardware range check turns into 0.0f -> the gather is branch free.
-    const float* in_base = G.in + (size_t)G.in_coff * HW;
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)in_base, (short)0, (int)0x80000000u, 0x00020000);
-    uint32_t poff[PJ];  // element offset of the lane's pixel (channel 0 of its frame)
-    int py[PJ], px[PJ];
-#pragma unroll
-    for (int j = 0; j < PJ; ++j) {
-        int p = p0 + j * 64 + lane;
-        const bool v = p < a.npix;
-        int pc = v ? p : 0;
-        int n = pc / HW;
-        int r = pc - n * HW;
-        py[j] = v ? r / a.W : -100000;  // out-of-range row => every tap invalid
-        px[j] = r - (r / a.W) * a.W;
-        poff[j] = (uint32_t)(n * G.in_cstride * HW + r);
-    }
-
-    const int nchunks = a.Kpad / KC;
-    const int c_begin = split * a.chunks_per_split;
-    const int c_end = min(nchunks, c_begin + a.chunks_per_split);
-
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
     const uint32_t HW4 = (uint32_t)HW * 4u;
-    // per-chunk gather state (computed once per chunk)
-    uint32_t base[PJ];
-    int ch0 = 0;
-
-    auto chunk_setup = [&](int c) __attribute__((always_inline)) {
-        if constexpr (TAP) {
-            const int cpt = a.Kpad / (KC * ks * ks);  // chunks per tap (wave-uniform scalars)
-            const int tap = c / cpt;
-            ch0 = (c - tap * cpt) * KC + wave * RW;
-            const int ky = tap / ks;
-            const int dy = ky - a.pad, dx = tap - ky * ks - a.pad;
-            const int shift = dy * a.W + dx;
-#pragma unroll
-            for (int j = 0; j < PJ; ++j) {
-                const int iy = py[j] + dy, ix = px[j] + dx;
-                const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-                // invalid taps start at 3 GiB: every row offset stays >= 2 GiB = num_records -> 0.0f
-                base[j] = ok ? (poff[j] + (uint32_t)shift) * 4u : 0xC0000000u;
-            }
-        }
-    };
-    // issue the LDS-DMA of B row r (this wave's) of chunk c into stage `buf`
-    auto dma_b_row = [&](int c, int buf, int r) __attribute__((always_inline)) {
-        if (a.ablate & 1) return;
-        float* Bs = lds + buf * (A_SZ + B_SZ) + A_SZ + (wave * RW + r) * PT;
-        if constexpr (TAP) {
-            const int ch = min(ch0 + r, a.Cin - 1);  // padded channels: any valid address (weights are 0)
-            const uint32_t choff = (uint32_t)ch * HW4;
-#pragma unroll
-            for (int j = 0; j < PJ; ++j)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + j * 64), 4, base[j] + choff, 0, 0, 0);
-        } else {
-            const int code = ktab[c * KC + wave * RW + r];  // (c << 8) | (ky << 4) | kx
-            const int cch = code >> 8;
-            const int dy = ((code >> 4) & 15) - a.pad;
-            const int dx = (code & 15) - a.pad;
-            const int delta = cch * HW + dy * a.W + dx;
-#pragma unroll
-            for (int j = 0; j < PJ; ++j) {
-                const int iy = py[j] + dy, ix = px[j] + dx;
-                const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-                const uint32_t off = ok ? (poff[j] + (uint32_t)delta) * 4u : 0xC0000000u;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + j * 64), 4, off, 0, 0, 0);
-            }
-        }
-    };
-    auto dma_a = [&](int c, int buf) __attribute__((always_inline)) {
-        if (a.ablate & 2) return;
-        const int k0 = c * KC;
-        float* As = lds + buf * (A_SZ + B_SZ);
-#pragma unroll
-        for (int i = 0; i < A_PW; ++i) {
-            const int piece = wave * A_PW + i;
-            const int f = piece * 256 + lane * 4;
-            const int row = f / MT, col = f - row * MT;
-            __builtin_amdgcn_global_load_lds((const void*)(G.wt + (size_t)(k0 + row) * a.Mpad + m0 + col),
-                                             (lds_ptr_t)(As + piece * 256), 16, 0, 0);
-        }
-    };
-
+    float* s_bias = lds + 2 * (A_SZ + B_SZ);
     const int wm0 = (wave & 1) * WM;
     const int wp0 = (wave >> 1) * WP;
 
-    if (c_begin < c_end) {
+    // Stream-K: the (tile, k-chunk) iteration space is cut into gridDim.x equal contiguous
+    // ranges, one per workgroup, so every CU gets the same work whatever the tile count
+    // (a data-parallel grid of 472 tiles on 512 slots leaves 8 % of the chip idle and a
+    // single-frame layer far more).  Ranges are XCD-contiguous (guide T1, bijective form):
+    // tiles sharing im2col halo rows or a pixel tile's M-tiles share an L2.  A tile split over
+    // several workgroups leaves float32 partials that conv_sk_fixup sums in k order.
+    const int Gw = gridDim.x;
+    const int b = blockIdx.x;
+    const int q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
+    const int id = xcd * q + min(xcd, rr) + (b >> 3);
+    const long long I = (long long)nM * nP * a.ngroups * nK;
+    const long long lo = (long long)id * I / Gw, hi = (long long)(id + 1) * I / Gw;
+
+    int first = 1;
+    for (long long itp = lo; itp < hi;) {
+        const int tile = (int)(itp / nK);
+        const int c_begin = (int)(itp - (long long)tile * nK);
+        const int c_end = (int)min<long long>(nK, c_begin + (hi - itp));
+        itp += c_end - c_begin;
+        const int mt = tile % nM;
+        const int rest = tile / nM;
+        const int pt = rest % nP;
+        const int g = rest / nP;
+        const ConvGroup G = g == 0 ? a.g[0] : a.g[1];  // no dynamic kernarg indexing
+        const int p0 = pt * PT;
+        const int m0 = mt * MT;
+
+        __syncthreads();  // the previous segment's epilogue is done with s_bias / the stages
+        if (tid < MT) s_bias[tid] = (m0 + tid < G.cout) ? G.bias[m0 + tid] : 0.f;
+
+        // ---- per-lane pixel state for the im2col gather.  The activation is read through a
+        // buffer resource: an invalid (zero-padding) tap gets a byte offset >= num_records,
+        // which the hardware range check turns into 0.0f -> the gather is branch free.
+        const float* in_base = G.in + (size_t)G.in_coff * HW;
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc((void*)in_base, (short)0, (int)0x80000000u, 0x00020000);
+        uint32_t poff[PJ];  // element offset of the lane's pixel (channel 0 of its frame)
+        int py[PJ], px[PJ];
+#pragma unroll
+        for (int j = 0; j < PJ; ++j) {
+            int p = p0 + j * 64 + lane;
+            const bool v = p < a.npix;
+            int pc = v ? p : 0;
+            int n = pc / HW;
+            int r = pc - n * HW;
+            py[j] = v ? r / a.W : -100000;  // out-of-range row => every tap invalid
+            px[j] = r - (r / a.W) * a.W;
+            poff[j] = (uint32_t)(n * G.in_cstride * HW + r);
+        }
+
+        floatx16 acc[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+        // per-chunk gather state (computed once per chunk)
+        uint32_t base[PJ];
+        int ch0 = 0;
+
+        auto chunk_setup = [&](int c) __attribute__((always_inline)) {
+            if constexpr (TAP) {
+                const int cpt = a.Kpad / (KC * ks * ks);  // chunks per tap (wave-uniform scalars)
+                const int tap = c / cpt;
+                ch0 = (c - tap * cpt) * KC + wave * RW;
+                const int ky = tap / ks;
+                const int dy = ky - a.pad, dx = tap - ky * ks - a.pad;
+                const int shift = dy * a.W + dx;
+#pragma unroll
+                for (int j = 0; j < PJ; ++j) {
+                    const int iy = py[j] + dy, ix = px[j] + dx;
+                    const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+                    // invalid taps start at 3 GiB: every row offset stays >= 2 GiB = num_records -> 0.0f
+                    base[j] = ok ? (poff[j] + (uint32_t)shift) * 4u : 0xC0000000u;
+                }
+            }
+        };
+        // issue the LDS-DMA of B row r (this wave's) of chunk c into stage `buf`
+        auto dma_b_row = [&](int c, int buf, int r) __attribute__((always_inline)) {
+            if constexpr ((ABL & 1) != 0) return;
+            float* Bs = lds + buf * (A_SZ + B_SZ) + A_SZ + (wave * RW + r) * PT;
+            if constexpr (TAP) {
+                const int ch = min(ch0 + r, a.Cin - 1);  // padded channels: any valid address (weights are 0)
+                const uint32_t choff = (uint32_t)ch * HW4;
+#pragma unroll
+                for (int j = 0; j < PJ; ++j)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + j * 64), 4, base[j] + choff, 0, 0,
+                                                            0);
+            } else {
+                const int code = ktab[c * KC + wave * RW + r];  // (c << 8) | (ky << 4) | kx
+                const int cch = code >> 8;
+                const int dy = ((code >> 4) & 15) - a.pad;
+                const int dx = (code & 15) - a.pad;
+                const int delta = cch * HW + dy * a.W + dx;
+#pragma unroll
+                for (int j = 0; j < PJ; ++j) {
+                    const int iy = py[j] + dy, ix = px[j] + dx;
+                    const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+                    const uint32_t off = ok ? (poff[j] + (uint32_t)delta) * 4u : 0xC0000000u;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + j * 64), 4, off, 0, 0, 0);
+                }
+            }
+        };
+        auto dma_a = [&](int c, int buf) __attribute__((always_inline)) {
+            if constexpr ((ABL & 2) != 0) return;
+            const int k0 = c * KC;
+            float* As = lds + buf * (A_SZ + B_SZ);
+#pragma unroll
+            for (int i = 0; i < A_PW; ++i) {
+                const int piece = wave * A_PW + i;
+                const int f = piece * 256 + lane * 4;
+                const int row = f / MT, col = f - row * MT;
+                __builtin_amdgcn_global_load_lds((const void*)(G.wt + (size_t)(k0 + row) * a.Mpad + m0 + col),
+                                                 (lds_ptr_t)(As + piece * 256), 16, 0, 0);
+            }
+        };
+
         chunk_setup(c_begin);
         dma_a(c_begin, 0);
 #pragma unroll
@@ -194,67 +202,117 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
             // chunk's B rows are issued one per k-step, between this chunk's MFMAs
             float av[2][TM], bv[2][TN];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) av[0][i] = As[hk * MT + i * 32];
+            for (int i = 0; i < TM; ++i) av[0][i] = (ABL & 4) ? (float)(lane + i) : As[hk * MT + i * 32];
 #pragma unroll
-            for (int j = 0; j < TN; ++j) bv[0][j] = Bs[hk * PT + j * 32];
+            for (int j = 0; j < TN; ++j) bv[0][j] = (ABL & 4) ? (float)(lane - j) : Bs[hk * PT + j * 32];
 #pragma unroll
-            for (int ks = 0; ks < KC / 2; ++ks) {
-                const int cur = ks & 1, nxt = cur ^ 1;
-                if (ks + 1 < KC / 2) {
-                    const int kr = 2 * (ks + 1) + hk;
+            for (int ks2 = 0; ks2 < KC / 2; ++ks2) {
+                const int cur = ks2 & 1, nxt = cur ^ 1;
+                if (ks2 + 1 < KC / 2) {
+                    const int kr = 2 * (ks2 + 1) + hk;
 #pragma unroll
-                    for (int i = 0; i < TM; ++i) av[nxt][i] = As[kr * MT + i * 32];
+                    for (int i = 0; i < TM; ++i) av[nxt][i] = (ABL & 4) ? av[cur][i] * 0.5f : As[kr * MT + i * 32];
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) bv[nxt][j] = Bs[kr * PT + j * 32];
+                    for (int j = 0; j < TN; ++j) bv[nxt][j] = (ABL & 4) ? bv[cur][j] * 0.5f : Bs[kr * PT + j * 32];
                 }
-                if (ks < RW && more) dma_b_row(c + 1, buf ^ 1, ks);
+                if (ks2 < RW && more) dma_b_row(c + 1, buf ^ 1, ks2);
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
-                if (ks + 1 < KC / 2) {
+                if (ks2 + 1 < KC / 2) {
                     // keep the next step's LDS reads ahead of this step's MFMAs
                     __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
                     __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
                 }
             }
-            __syncthreads();  // next stage landed everywhere; this stage free for reuse
+            if constexpr ((ABL & 8) == 0) __syncthreads();  // next stage landed everywhere; this stage free
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-    }
 
-    // ---- epilogue
+        // ---- epilogue: whole tile -> bias + ReLU into the channel slice; part of a tile ->
+        // float32 partial slab [MT][PT] in slot 2*id (first segment) or 2*id+1 (last)
+        const bool whole = c_begin == 0 && c_end == nK;
+        float* slab = a.partial + (size_t)(2 * id + (first ? 0 : 1)) * (MT * PT);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int p = p0 + wp0 + j * 32 + l31;
-        if (p >= a.npix) continue;
-        if (a.splits > 1) {
-            float* slab = a.partial + ((size_t)(g * a.splits + split) * a.Mpad) * a.npix + p;
+        for (int j = 0; j < TN; ++j) {
+            const int pl = wp0 + j * 32 + l31;
+            const int p = p0 + pl;
+            if (!whole) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int ml = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
+                        slab[ml * PT + pl] = acc[i][j][r];
+                    }
+                continue;
+            }
+            if (p >= a.npix) continue;
+            const int n = p / HW;
+            const int rem = p - n * HW;
+            float* ob = G.out + ((size_t)n * G.out_cstride + G.out_coff) * HW + rem;
+            float* ob2 = G.out2 ? G.out2 + ((size_t)n * G.out2_cstride + G.out2_coff) * HW + rem : nullptr;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-                    slab[(size_t)m * a.npix] = acc[i][j][r];
+                    if (m < G.cout) {
+                        float v = acc[i][j][r] + s_bias[m - m0];
+                        if (G.relu) v = fmaxf(v, 0.f);
+                        ob[(size_t)m * HW] = v;
+                        if (ob2) ob2[(size_t)m * HW] = v;
+                    }
                 }
-            continue;
         }
+        first = 0;
+    }
+}
+
+// Stream-K fixup: grid (tiles, MT*PT/1024); each thread finishes 4 consecutive pixels of one
+// output channel of a tile that several workgroups shared: partial slabs summed in k order
+// (deterministic), + bias, ReLU, written into the channel slice.
+template <int MT, int PT>
+__global__ __launch_bounds__(256) void conv_sk_fixup(ConvArgs a) {
+    const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
+    const int nK = a.Kpad / KC;
+    const long long Gw = a.sk_grid;
+    const long long I = (long long)nM * nP * a.ngroups * nK;
+    const int tile = blockIdx.x;
+    const long long x0 = (long long)tile * nK;
+    const int w0 = (int)(((x0 + 1) * Gw - 1) / I);       // workgroup whose range holds x0
+    const int w1 = (int)(((x0 + nK) * Gw - 1) / I);      // ... holds the tile's last chunk
+    if (w0 == w1) return;  // one workgroup computed the whole tile and wrote it directly
+    const int mt = tile % nM;
+    const int rest = tile / nM;
+    const int pt = rest % nP;
+    const int g = rest / nP;
+    const ConvGroup G = g == 0 ? a.g[0] : a.g[1];
+    const int HW = a.H * a.W;
+    const int e = (blockIdx.y * 256 + threadIdx.x) * 4;
+    const int ml = e / PT, pl = e - ml * PT;
+    const int m = mt * MT + ml;
+    if (m >= G.cout) return;
+    f32x4 v;
+    for (int w = w0; w <= w1; ++w) {
+        const long long lo_w = (long long)w * I / Gw;
+        const int slot = (lo_w / nK == tile) ? 2 * w : 2 * w + 1;
+        const f32x4 part = *reinterpret_cast<const f32x4*>(a.partial + (size_t)slot * (MT * PT) + e);
+        v = (w == w0) ? part : v + part;
+    }
+    const float bias = G.bias[m];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int p = pt * PT + pl + k;
+        if (p >= a.npix) break;
+        float o = v[k] + bias;
+        if (G.relu) o = fmaxf(o, 0.f);
         const int n = p / HW;
         const int rem = p - n * HW;
-        float* ob = G.out + ((size_t)n * G.out_cstride + G.out_coff) * HW + rem;
-        float* ob2 = G.out2 ? G.out2 + ((size_t)n * G.out2_cstride + G.out2_coff) * HW + rem : nullptr;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-                if (m < G.cout) {
-                    float v = acc[i][j][r] + s_bias[m - m0];
-                    if (G.relu) v = fmaxf(v, 0.f);
-                    ob[(size_t)m * HW] = v;
-                    if (ob2) ob2[(size_t)m * HW] = v;
-                }
-            }
+        G.out[((size_t)n * G.out_cstride + G.out_coff + m) * HW + rem] = o;
+        if (G.out2) G.out2[((size_t)n * G.out2_cstride + G.out2_coff + m) * HW + rem] = o;
     }
 }
 
@@ -271,27 +329,6 @@ __global__ void fill_hash(float* p, size_t n, uint32_t seed) {
 
 void launch_fill_hash(float* p, size_t n, uint32_t seed, hipStream_t st) {
     hipLaunchKernelGGL(fill_hash, dim3(2048), dim3(256), 0, st, p, n, seed);
-}
-
-// Deterministic split-K combine: slabs summed in split order, then bias + ReLU.
-__global__ __launch_bounds__(256) void conv_splitk_reduce(ConvArgs a) {
-    const int g = blockIdx.y;
-    const ConvGroup G = g == 0 ? a.g[0] : a.g[1];
-    const int HW = a.H * a.W;
-    const size_t total = (size_t)G.cout * a.npix;
-    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
-        const int m = (int)(e / a.npix);
-        const int p = (int)(e - (size_t)m * a.npix);
-        const float* s = a.partial + ((size_t)g * a.splits * a.Mpad + m) * a.npix + p;
-        float v = s[0];
-        for (int k = 1; k < a.splits; ++k) v += s[(size_t)k * a.Mpad * a.npix];
-        v += G.bias[m];
-        if (G.relu) v = fmaxf(v, 0.f);
-        const int n = p / HW;
-        const int rem = p - n * HW;
-        G.out[((size_t)n * G.out_cstride + G.out_coff + m) * HW + rem] = v;
-        if (G.out2) G.out2[((size_t)n * G.out2_cstride + G.out2_coff + m) * HW + rem] = v;
-    }
 }
 
 // MaxPool2d(2, 2), floor mode (src/model.py:10-13); NCHW, C channels contiguous planes.
@@ -311,8 +348,8 @@ __global__ __launch_bounds__(256) void maxpool2x2(const float* __restrict__ in, 
 
 // ------------------------------------------------------------------ host launchers
 template <int MT, int PT>
-static void launch_tile(const ConvArgs& a, int ngroups, const int* ktab, hipStream_t st) {
-    dim3 grid(((a.npix + PT - 1) / PT) * (a.Mpad / MT) * ngroups * a.splits);
+static void launch_tile(const ConvArgs& a, const int* ktab, hipStream_t st) {
+    const dim3 grid(a.sk_grid);
     if (!a.tap_major)
         hipLaunchKernelGGL((conv_igemm_f32<MT, PT, false, 0>), grid, dim3(NT), 0, st, a, ktab);
     else if (a.ks == 7)
@@ -323,20 +360,28 @@ static void launch_tile(const ConvArgs& a, int ngroups, const int* ktab, hipStre
         hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 1>), grid, dim3(NT), 0, st, a, ktab);
     else
         hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 0>), grid, dim3(NT), 0, st, a, ktab);
+    const int tiles = (a.Mpad / MT) * ((a.npix + PT - 1) / PT) * a.ngroups;
+    if (a.sk_grid != tiles)
+        hipLaunchKernelGGL((conv_sk_fixup<MT, PT>), dim3(tiles, MT * PT / 1024), dim3(256), 0, st, a);
 }
 
-void launch_conv(const ConvArgs& a, int ngroups, const int* ktab, int mt, int pt, hipStream_t st) {
-    if (mt == 128 && pt == 128) launch_tile<128, 128>(a, ngroups, ktab, st);
-    else if (mt == 128 && pt == 64) launch_tile<128, 64>(a, ngroups, ktab, st);
-    else if (mt == 64 && pt == 128) launch_tile<64, 128>(a, ngroups, ktab, st);
-    else launch_tile<64, 64>(a, ngroups, ktab, st);
-    if (a.splits > 1) {
-        size_t total = 0;
-        for (int g = 0; g < ngroups; ++g) total = total > (size_t)a.g[g].cout * a.npix ? total : (size_t)a.g[g].cout * a.npix;
-        int blocks = (int)((total + 255) / 256);
-        if (blocks > 2048) blocks = 2048;
-        hipLaunchKernelGGL(conv_splitk_reduce, dim3(blocks, ngroups), dim3(256), 0, st, a);
+void launch_conv_ablation(const ConvArgs& a, int ablate, hipStream_t st) {
+    const dim3 grid(a.sk_grid);
+    switch (ablate) {
+        case 3: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 3>), grid, dim3(NT), 0, st, a, nullptr); break;
+        case 7: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 7>), grid, dim3(NT), 0, st, a, nullptr); break;
+        case 11: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 11>), grid, dim3(NT), 0, st, a, nullptr); break;
+        case 15: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 15>), grid, dim3(NT), 0, st, a, nullptr); break;
+        case 1: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 1>), grid, dim3(NT), 0, st, a, nullptr); break;
+        default: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 2>), grid, dim3(NT), 0, st, a, nullptr); break;
     }
+}
+
+void launch_conv(const ConvArgs& a, const int* ktab, int mt, int pt, hipStream_t st) {
+    if (mt == 128 && pt == 128) launch_tile<128, 128>(a, ktab, st);
+    else if (mt == 128 && pt == 64) launch_tile<128, 64>(a, ktab, st);
+    else if (mt == 64 && pt == 128) launch_tile<64, 128>(a, ktab, st);
+    else launch_tile<64, 64>(a, ktab, st);
 }
 
 void launch_maxpool(const float* in, float* out, int NC, int H, int W, hipStream_t st) {

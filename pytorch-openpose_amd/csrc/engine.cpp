@@ -222,34 +222,42 @@ struct Act {  // a channel slice of an NCHW activation buffer
 
 // --------------------------------------------------------------- conv launch planning
 struct TileChoice {
-    int mt, pt, splits, cps;
+    int mt, pt, grid;  // tile shape, workgroups (grid == tiles: data parallel; else stream-K)
 };
 
-TileChoice choose_tile(int Mpad, int npix, int ngroups, int nchunks) {
-    // Cost model in units of one 32-deep k-chunk of a 64x64 tile on one CU (~0.42 us at
-    // the fp32 MFMA rate).  A CU running k >= 2 co-resident workgroups finishes them in
-    // k * work; a lone workgroup (one wave per SIMD) only reaches ~60 % of the MFMA rate.
-    static const int cfg[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+// Cost model in units of one 32-deep k-chunk of a 64x64 output tile on one CU.  A CU that
+// holds k >= 2 co-resident workgroups finishes them in k * work; a lone workgroup (one wave per
+// SIMD) runs at ~60 %.  Stream-K (grid = all resident slots) balances the chip exactly and
+// pays for the partial slabs of tiles it splits plus one fixup launch.
+TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK) {
+    static const int cfg[4][3] = {{128, 128, 2}, {128, 64, 3}, {64, 128, 3}, {64, 64, 4}};  // mt, pt, WG/CU
     static const double ovh[4] = {1.0, 1.10, 1.10, 1.30};  // load/issue overhead per MFMA
-    TileChoice best{64, 64, 1, nchunks};
+    TileChoice best{64, 64, 1};
     double best_cost = 1e300;
     for (int c = 0; c < 4; ++c) {
-        const int mt = cfg[c][0], pt = cfg[c][1];
+        const int mt = cfg[c][0], pt = cfg[c][1], occ = cfg[c][2];
         if (Mpad % mt) continue;
         const long tiles = (long)(Mpad / mt) * ((npix + pt - 1) / pt) * ngroups;
-        for (int s = 1; s <= 64; s *= 2) {
-            const int cps = (nchunks + s - 1) / s;
-            if (s > 1 && cps < 4) break;
-            const long wgs = tiles * s;
-            const double per_cu = std::max<double>((wgs + 255) / 256, 1.6);
-            double cost = per_cu * cps * (mt / 64.0) * (pt / 64.0) * ovh[c];
-            if (s > 1) {  // slab write + ordered re-read + one extra launch (~2 us)
-                const double bytes = 8.0 * s * Mpad * (double)npix * ngroups;
-                cost += bytes / 5e12 / 0.42e-6 + 5.0;
-            }
-            if (cost < best_cost * 0.97) {
-                best_cost = cost;
-                best = {mt, pt, s, cps};
+        const double unit = (mt / 64.0) * (pt / 64.0) * ovh[c];
+        // data parallel
+        const long per_cu = (tiles + 255) / 256;
+        const double dp = std::max<double>(per_cu, 1.6) * nK * unit;
+        if (dp < best_cost * 0.97) {
+            best_cost = dp;
+            best = {mt, pt, (int)tiles};
+        }
+        // stream-K over every resident slot (each workgroup >= 4 chunks)
+        const long iters = tiles * nK;
+        long grid = std::min<long>(256L * occ, iters / 4);
+        if (grid >= 1 && grid != tiles) {
+            const double per_wg = (double)iters / grid;
+            const double cu_load = std::max(1.6, std::ceil(grid / 256.0)) * per_wg * unit;
+            const long split = std::min<long>(tiles, 2 * grid);                 // tiles with partials
+            const double slab_bytes = (double)split * mt * pt * 4.0 * 3.0;       // write + re-read + out
+            const double sk = cu_load + slab_bytes / 5e12 / 0.42e-6 + 8.0;      // + fixup launch
+            if (sk < best_cost * 0.97) {
+                best_cost = sk;
+                best = {mt, pt, (int)grid};
             }
         }
     }
@@ -356,17 +364,17 @@ static void run_conv(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W
         if ((double)N * ins[g].cstride * H * W * 4.0 >= 2147483648.0)
             throw std::invalid_argument("activation slab >= 2 GiB: split the batch");
     const TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.Kpad / 32);
-    a.splits = t.splits;
-    a.chunks_per_split = t.cps;
-    if (t.splits > 1) a.partial = h->partial.ensure<float>((size_t)ng * t.splits * a.Mpad * a.npix, h->stream);
+    a.ngroups = ng;
+    a.sk_grid = t.grid;
+    a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
     double flops = 0;
     for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)a.K * a.npix;
     ProfEntry pe;
     h->prof_begin(pe, conv_class(c0->ks), flops, 0);
     if (h->detail)
         pe.detail = "layer/" + c0->name + "/" + std::to_string(t.mt) + "x" + std::to_string(t.pt) + "s" +
-                    std::to_string(t.splits) + "/n" + std::to_string(a.npix);
-    launch_conv(a, ng, c0->ktab, t.mt, t.pt, h->stream);
+                    std::to_string(t.grid) + "/n" + std::to_string(a.npix);
+    launch_conv(a, c0->ktab, t.mt, t.pt, h->stream);
     h->prof_end(pe);
 }
 
@@ -968,12 +976,13 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
         G.out = yd; G.out_cstride = Cout; G.out_coff = 0; G.out2 = nullptr; G.cout = Cout; G.relu = relu;
         a.g[1] = a.g[0];
         TileChoice t = choose_tile(a.Mpad, a.npix, 1, a.Kpad / 32);
-        if (mt > 0) { t.mt = mt; t.pt = pt; }
-        if (splits > 0) { t.splits = splits; t.cps = (a.Kpad / 32 + splits - 1) / splits; }
+        if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((a.npix + pt - 1) / pt); }
+        if (splits > 0) t.grid = splits;
         if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
-        a.splits = t.splits; a.chunks_per_split = t.cps;
-        if (t.splits > 1) a.partial = h->partial.ensure<float>((size_t)t.splits * a.Mpad * a.npix, h->stream);
-        launch_conv(a, 1, c->ktab, t.mt, t.pt, h->stream);
+        a.ngroups = 1;
+        a.sk_grid = t.grid;
+        a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        launch_conv(a, c->ktab, t.mt, t.pt, h->stream);
         OPOSE_HIP_CHECK(hipMemcpyAsync(out, yd, ny * 4, hipMemcpyDeviceToHost, h->stream));
         OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
         h->convs[0].erase("__debug__");
@@ -1001,7 +1010,6 @@ int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, in
         a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.ks = ks; a.pad = ks / 2;
         a.K = c->K; a.Kpad = c->Kpad; a.Mpad = c->Mpad; a.npix = N * H * W;
         a.tap_major = c->tap_major ? 1 : 0;
-        a.ablate = ablate;
         for (int g = 0; g < 2; ++g) {
             ConvGroup& G = a.g[g];
             const int gg = g < ngroups ? g : 0;
@@ -1010,17 +1018,27 @@ int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, in
             G.cout = Cout; G.relu = 1;
         }
         TileChoice t = choose_tile(a.Mpad, a.npix, ngroups, a.Kpad / 32);
-        if (mt > 0) { t.mt = mt; t.pt = pt; }
-        if (splits > 0) { t.splits = splits; t.cps = (a.Kpad / 32 + splits - 1) / splits; }
+        if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((a.npix + pt - 1) / pt) * ngroups; }
+        if (splits > 0) t.grid = splits;
         if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
-        a.splits = t.splits; a.chunks_per_split = t.cps;
-        if (t.splits > 1) a.partial = h->partial.ensure<float>((size_t)ngroups * t.splits * a.Mpad * a.npix, h->stream);
-        launch_conv(a, ngroups, c->ktab, t.mt, t.pt, h->stream);  // warm-up
+        a.ngroups = ngroups;
+        a.sk_grid = t.grid;
+        a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        auto go = [&]() {
+            if (ablate) {
+                if (!(a.tap_major && a.ks == 7 && t.mt == 128 && t.pt == 128))
+                    throw std::invalid_argument("ablations exist for the 128x128 7x7 kernel only");
+                launch_conv_ablation(a, ablate, h->stream);
+            } else {
+                launch_conv(a, c->ktab, t.mt, t.pt, h->stream);
+            }
+        };
+        go();  // warm-up
         hipEvent_t e0, e1;
         OPOSE_HIP_CHECK(hipEventCreate(&e0));
         OPOSE_HIP_CHECK(hipEventCreate(&e1));
         OPOSE_HIP_CHECK(hipEventRecord(e0, h->stream));
-        for (int r = 0; r < reps; ++r) launch_conv(a, ngroups, c->ktab, t.mt, t.pt, h->stream);
+        for (int r = 0; r < reps; ++r) go();
         OPOSE_HIP_CHECK(hipEventRecord(e1, h->stream));
         OPOSE_HIP_CHECK(hipEventSynchronize(e1));
         OPOSE_HIP_CHECK(hipEventElapsedTime(ms, e0, e1));

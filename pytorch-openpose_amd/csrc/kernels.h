@@ -20,7 +20,8 @@ struct Conn {
 };
 
 // conv.hip
-void launch_conv(const ConvArgs& a, int ngroups, const int* ktab, int mt, int pt, hipStream_t st);
+void launch_conv(const ConvArgs& a, const int* ktab, int mt, int pt, hipStream_t st);
+void launch_conv_ablation(const ConvArgs& a, int ablate, hipStream_t st);
 void launch_fill_hash(float* p, size_t n, uint32_t seed, hipStream_t st);
 void launch_maxpool(const float* in, float* out, int NC, int H, int W, hipStream_t st);
 

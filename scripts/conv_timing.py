@@ -15,8 +15,8 @@ cases = [  # name, N, Cin, H, W, Cout, ks, ngroups
     ("conv1_2", 32, 64, 184, 328, 64, 3, 1),
     ("Mconv2 1 frame", 1, 128, 23, 41, 128, 7, 2),
 ]
-variants = [(0, 0, 0, 0), (128, 128, 1, 0), (128, 128, 1, 1), (128, 128, 1, 2), (128, 128, 1, 3),
-            (64, 128, 1, 0), (128, 64, 1, 0), (64, 64, 1, 0)]
+variants = [(0, 0, 0, 0), (128, 128, 0, 0), (128, 128, 512, 0), (128, 128, 0, 3), (128, 128, 512, 3),
+            (64, 128, 0, 0), (128, 64, 0, 0), (64, 64, 0, 0)]
 only = sys.argv[1:] or None
 for name, N, Cin, H, W, Cout, ks, ng in cases:
     flops = 2.0 * N * H * W * Cout * Cin * ks * ks * ng
