@@ -15,6 +15,7 @@ Usage:  PYTHONDONTWRITEBYTECODE=1 python -m oracle.gen_golden
 """
 from __future__ import annotations
 
+import glob
 import json
 import os
 import shutil
@@ -202,5 +203,27 @@ def main():
                    "resize": "cv2.resize routed through oracle.cv_resize (OpenCV parity unpinned)"}, f, indent=1)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+def gen_hand_detect():
+    """util.handDetect (src/util.py:133-201) on the planted Body fixtures' outputs."""
+    from src import util as ref_util
+    cases = []
+    for p in sorted(glob.glob(os.path.join(OUT, "body_planted_*.npz"))):
+        d = np.load(p)
+        if d["subset"].shape[0] == 0:
+            continue
+        H, W = (int(v) for v in d["img_hw"])
+        boxes = ref_util.handDetect(d["candidate"], d["subset"], np.zeros((H, W, 3), np.uint8))
+        cases.append({"fixture": os.path.basename(p), "boxes": [[int(x), int(y), int(w), bool(l)] for x, y, w, l in boxes]})
+    with open(os.path.join(OUT, "hand_detect.json"), "w") as f:
+        json.dump(cases, f, indent=0)
+    print("wrote hand_detect.json", len(cases))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "hand_detect":
+    install_shims()
+    sys.path.insert(0, REF)
+    gen_hand_detect()
