@@ -551,15 +551,21 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
         launch_gauss_nms_fused(S, N, 38, p.thre1, cap, cnt, list, lscore, h->stream);
         h->prof_end(pe);
     } else {
+        // single scale: the float64 average equals the float32 resize output exactly -> f32 map
+        const bool f32 = ns == 1;
         double* avg = h->avg.ensure<double>((size_t)N * 18 * H * W, h->stream);
         for (int s = 0; s < ns; ++s) {
-            h->prof_begin(pe, "heat_full", 0, (double)N * 18 * H * W * 8 * (s ? 2 : 1));
-            launch_heat_full(S.mid[s], 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx, ns, s > 0,
-                             avg, h->stream);
+            h->prof_begin(pe, "heat_full", 0, (double)N * 18 * H * W * (f32 ? 4 : 8) * (s ? 2 : 1));
+            if (f32)
+                launch_heat_full_f32(S.mid[s], 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx,
+                                     reinterpret_cast<float*>(avg), h->stream);
+            else
+                launch_heat_full(S.mid[s], 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx, ns,
+                                 s > 0, avg, h->stream);
             h->prof_end(pe);
         }
-        h->prof_begin(pe, "gauss_nms", 0, (double)N * 18 * H * W * 8);
-        launch_gauss_nms(avg, N * 18, H, W, p.thre1, cap, cnt, list, lscore, h->stream);
+        h->prof_begin(pe, "gauss_nms", 0, (double)N * 18 * H * W * (f32 ? 4 : 8));
+        launch_gauss_nms(avg, f32, N * 18, H, W, p.thre1, cap, cnt, list, lscore, h->stream);
         h->prof_end(pe);
     }
     h->prof_begin(pe, "peaks_finalize", 0, 0);

@@ -82,9 +82,12 @@ __global__ __launch_bounds__(256) void upsample8(const float* __restrict__ in, i
 
 // cubic resize of mid [N][Cm][Hs][Ws] channels [coff, coff+P) to [H][W], then
 // avg[n][p] (+)= (double)(v / nscales)   (float32 divide, float64 accumulate).
+// T = float when there is a single scale: the average is then exactly the float32 resize
+// output (0.0 + (double)v), so the float64 map can be stored at half the bytes.
+template <typename T>
 __global__ __launch_bounds__(256) void heat_full_accum(const float* __restrict__ mid, int Cm, int coff, int P, int Hs,
                                                        int Ws, int H, int W, double scale_y, double scale_x,
-                                                       float nscales, int accumulate, double* __restrict__ avg) {
+                                                       float nscales, int accumulate, T* __restrict__ avg) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int np = blockIdx.z;
@@ -95,8 +98,9 @@ __global__ __launch_bounds__(256) void heat_full_accum(const float* __restrict__
     const float* plane = mid + ((size_t)n * Cm + coff + p) * Hs * Ws;
     float v = (Hs == H && Ws == W) ? plane[(size_t)y * Ws + x] : cubic_sample_f32(plane, Ws, ty, tx);
     v = v / nscales;
-    double* d = avg + ((size_t)np * H + y) * W + x;
-    *d = accumulate ? *d + (double)v : 0.0 + (double)v;
+    T* d = avg + ((size_t)np * H + y) * W + x;
+    if constexpr (sizeof(T) == 4) *d = 0.f + v;  // == (float)(0.0 + (double)v), incl. the sign of zero
+    else *d = accumulate ? *d + (double)v : 0.0 + (double)v;
 }
 
 void launch_preprocess(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int Hs,
@@ -115,8 +119,15 @@ void launch_upsample8(const float* in, int in_cstride, int in_coff, int C, int N
 void launch_heat_full(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
                       double sx, int nscales, int accumulate, double* avg, hipStream_t st) {
     dim3 grid((W + 255) / 256, H, N * P);
-    hipLaunchKernelGGL(heat_full_accum, grid, dim3(256), 0, st, mid, Cm, coff, P, Hs, Ws, H, W, sy, sx,
+    hipLaunchKernelGGL(heat_full_accum<double>, grid, dim3(256), 0, st, mid, Cm, coff, P, Hs, Ws, H, W, sy, sx,
                        (float)nscales, accumulate, avg);
+}
+
+void launch_heat_full_f32(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
+                          double sx, float* avg, hipStream_t st) {
+    dim3 grid((W + 255) / 256, H, N * P);
+    hipLaunchKernelGGL(heat_full_accum<float>, grid, dim3(256), 0, st, mid, Cm, coff, P, Hs, Ws, H, W, sy, sx, 1.f, 0,
+                       avg);
 }
 
 }  // namespace opose

@@ -32,9 +32,11 @@ void launch_upsample8(const float* in, int in_cstride, int in_coff, int C, int N
                       float* out, hipStream_t st);
 void launch_heat_full(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
                       double sx, int nscales, int accumulate, double* avg, hipStream_t st);
+void launch_heat_full_f32(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
+                          double sx, float* avg, hipStream_t st);
 
 // post.hip
-void launch_gauss_nms(const double* avg, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
+void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
                       double* list_score, hipStream_t st);
 void launch_gauss_nms_fused(const PafScales& S, int N, int ch0, double thre, int cap, int* cnt, int* list,
                             double* list_score, hipStream_t st);

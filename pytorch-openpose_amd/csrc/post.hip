@@ -89,14 +89,15 @@ __device__ __forceinline__ void gauss_passes(GaussTile& t) {
     __syncthreads();
 }
 
-__device__ __forceinline__ void gauss_tile(const double* __restrict__ m, int H, int W, int x0, int y0, GaussTile& t) {
+template <typename T>
+__device__ __forceinline__ void gauss_tile(const T* __restrict__ m, int H, int W, int x0, int y0, GaussTile& t) {
     constexpr int IIT = (GI * GI + 255) / 256;
     double iv[IIT];
 #pragma unroll
     for (int it = 0; it < IIT; ++it) {  // all loads of a thread in flight together
         const int e = min((int)threadIdx.x + it * 256, GI * GI - 1);
         const int r = e / GI, c = e - r * GI;
-        iv[it] = m[(size_t)reflect_idx(y0 - 13 + r, H) * W + reflect_idx(x0 - 13 + c, W)];
+        iv[it] = (double)m[(size_t)reflect_idx(y0 - 13 + r, H) * W + reflect_idx(x0 - 13 + c, W)];
     }
 #pragma unroll
     for (int it = 0; it < IIT; ++it) {
@@ -108,12 +109,20 @@ __device__ __forceinline__ void gauss_tile(const double* __restrict__ m, int H, 
 }
 
 // avg: [N*P][H][W] float64; one workgroup per GT x GT tile of one part of one frame.
-__global__ __launch_bounds__(256) void gauss_nms(const double* __restrict__ avg, int P, int H, int W, double thre,
+// 1-D grid over (x tile, y tile, map) with an XCD-contiguous order (guide T1): horizontally
+// and vertically adjacent tiles, which re-read each other's 13-pixel halos, share an L2.
+template <typename T>
+__global__ __launch_bounds__(256) void gauss_nms(const T* __restrict__ avg, int P, int H, int W, double thre,
                                                  int cap, int* __restrict__ cnt, int* __restrict__ list,
                                                  double* __restrict__ list_score) {
     __shared__ GaussTile t;
-    const int x0 = blockIdx.x * GT, y0 = blockIdx.y * GT;
-    const int np = blockIdx.z;
+    const int ntx = (W + GT - 1) / GT, nty = (H + GT - 1) / GT;
+    const int total = gridDim.x, b = blockIdx.x;
+    const int q = total >> 3, rr = total & 7, xcd = b & 7;
+    const int id = xcd * q + min(xcd, rr) + (b >> 3);
+    const int tx = id % ntx, rest = id / ntx;
+    const int ty = rest % nty, np = rest / nty;
+    const int x0 = tx * GT, y0 = ty * GT;
     gauss_tile(avg + (size_t)np * H * W, H, W, x0, y0, t);
     for (int e = threadIdx.x; e < GT * GT; e += 256) {
         const int r = e / GT, c = e - r * GT;
@@ -595,10 +604,15 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
 }
 
 // ------------------------------------------------------------------ launchers
-void launch_gauss_nms(const double* avg, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
+void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
                       double* list_score, hipStream_t st) {
-    dim3 grid((W + GT - 1) / GT, (H + GT - 1) / GT, NP);
-    hipLaunchKernelGGL(gauss_nms, grid, dim3(256), 0, st, avg, 18, H, W, thre, cap, cnt, list, list_score);
+    dim3 grid(((W + GT - 1) / GT) * ((H + GT - 1) / GT) * NP);
+    if (f32)
+        hipLaunchKernelGGL(gauss_nms<float>, grid, dim3(256), 0, st, (const float*)avg, 18, H, W, thre, cap, cnt, list,
+                           list_score);
+    else
+        hipLaunchKernelGGL(gauss_nms<double>, grid, dim3(256), 0, st, (const double*)avg, 18, H, W, thre, cap, cnt,
+                           list, list_score);
 }
 
 void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st) {

@@ -207,3 +207,36 @@ def test_body_call_surface_and_empty_frame(body):
     a = body(big[::1, 10:250])
     b = body(np.ascontiguousarray(big[:, 10:250]))
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_capacity_overflow_grows_and_matches(native):
+    """Records too small for the frame: the library flags OPOSE_E_CAPACITY, the facade grows
+    the capacity and re-runs; the result still equals the reference fixture."""
+    from src.body import Body
+    from src.weights import seeded_state_dict
+    small = Body(seeded_state_dict("body", 0), peaks_per_part=2, max_people=2)
+    for path in sorted(glob.glob(os.path.join(GOLDEN, "body_planted_5*_368x656_p14.npz")))[:2]:
+        d = np.load(path)
+        maps = np.concatenate([d["paf"], d["heat"]], 0)[None]
+        cand, subset = small.post(maps, list(d["pad"]), 368, 656)[0]
+        assert np.array_equal(cand, d["candidate"]) and np.array_equal(subset, d["subset"])
+    assert small.peaks_per_part > 2 and small.max_people > 2
+
+
+@pytest.mark.parametrize("hw", [(10, 12), (9, 40), (200, 11)])
+def test_tiny_frames_vs_oracle(body, hw):
+    """Frames smaller than the 25-tap Gaussian (scipy 'reflect' wraps more than once)."""
+    from oracle import body_post, network
+    sd = network.seeded_state_dict("body", 0)
+    img = np.random.default_rng(hw[0] * 7 + hw[1]).integers(0, 256, hw + (3,), dtype=np.uint8)
+
+    def net_fn(x):
+        p, h = network.body_forward(torch.from_numpy(x), sd)
+        return p.numpy(), h.numpy()
+
+    ref_c, ref_s = body_post.body_infer(img, net_fn)
+    cand, subset = body(img)
+    assert cand.shape == ref_c.shape and subset.shape == ref_s.shape
+    if cand.size:
+        assert np.array_equal(cand[:, [0, 1, 3]], ref_c[:, [0, 1, 3]])
+    assert np.array_equal(subset[:, :18], ref_s[:, :18])
