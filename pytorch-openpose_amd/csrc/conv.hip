@@ -191,41 +191,59 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
         __syncthreads();  // s_waitcnt vmcnt(0) + barrier: stage 0 landed for every wave
         for (int c = c_begin; c < c_end; ++c) {
             const int buf = (c - c_begin) & 1;
-            const bool more = c + 1 < c_end;
-            if (more) {
-                chunk_setup(c + 1);
-                dma_a(c + 1, buf ^ 1);
-            }
-            const float* As = lds + buf * (A_SZ + B_SZ) + wm0 + l31;
-            const float* Bs = lds + buf * (A_SZ + B_SZ) + A_SZ + wp0 + l31;
-            // fragments of k-step ks+1 are read while the MFMAs of k-step ks run; the next
-            // chunk's B rows are issued one per k-step, between this chunk's MFMAs
+            // the last chunk re-issues its own DMA into the free stage instead of branching:
+            // a branch-free loop body lets the compiler keep the LDS reads 2 deep (lgkmcnt(2))
+            const int cn = min(c + 1, c_end - 1);
+            chunk_setup(cn);
+            dma_a(cn, buf ^ 1);
+            // Fragment reads are explicit ds_read_b32 with immediate offsets and counted waits:
+            // the reads of k-step ks+1 are issued in front of k-step ks's MFMAs and waited for
+            // with lgkmcnt(TM+TN) (LDS returns in order), so they have a whole k-step to land.
+            // (Compiler-visible reads get lgkmcnt(0) once LDS-DMA is in flight, which stalls
+            // the wave on the reads it has only just issued.)
+            const uint32_t a_lds = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_SZ + B_SZ) + wm0 + l31 + hk * MT);
+            const uint32_t b_lds =
+                (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_SZ + B_SZ) + A_SZ + wp0 + l31 + hk * PT);
             float av[2][TM], bv[2][TN];
+            auto read_frags = [&](int step, float (&fa)[TM], float (&fb)[TN]) __attribute__((always_inline)) {
 #pragma unroll
-            for (int i = 0; i < TM; ++i) av[0][i] = (ABL & 4) ? (float)(lane + i) : As[hk * MT + i * 32];
+                for (int i = 0; i < TM; ++i) {
+                    if constexpr ((ABL & 4) != 0) fa[i] = (float)(lane + i + step);
+                    else
+                        asm volatile("ds_read_b32 %0, %1 offset:%2"
+                                     : "=v"(fa[i])
+                                     : "v"(a_lds), "i"((2 * step * MT + i * 32) * 4));
+                }
 #pragma unroll
-            for (int j = 0; j < TN; ++j) bv[0][j] = (ABL & 4) ? (float)(lane - j) : Bs[hk * PT + j * 32];
+                for (int j = 0; j < TN; ++j) {
+                    if constexpr ((ABL & 4) != 0) fb[j] = (float)(lane - j - step);
+                    else
+                        asm volatile("ds_read_b32 %0, %1 offset:%2"
+                                     : "=v"(fb[j])
+                                     : "v"(b_lds), "i"((2 * step * PT + j * 32) * 4));
+                }
+            };
+            read_frags(0, av[0], bv[0]);
 #pragma unroll
             for (int ks2 = 0; ks2 < KC / 2; ++ks2) {
                 const int cur = ks2 & 1, nxt = cur ^ 1;
-                if (ks2 + 1 < KC / 2) {
-                    const int kr = 2 * (ks2 + 1) + hk;
+                if (ks2 + 1 < KC / 2) read_frags(ks2 + 1, av[nxt], bv[nxt]);
+                if (ks2 < RW) dma_b_row(cn, buf ^ 1, ks2);
+                // wait for this step's fragments only (the next step's stay in flight); the "+v"
+                // operands order the MFMAs after the wait
+                if constexpr ((ABL & 4) == 0) {
+                    if (ks2 + 1 < KC / 2) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TM + TN));
+                    else asm volatile("s_waitcnt lgkmcnt(0)");
 #pragma unroll
-                    for (int i = 0; i < TM; ++i) av[nxt][i] = (ABL & 4) ? av[cur][i] * 0.5f : As[kr * MT + i * 32];
+                    for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(av[cur][i]));
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) bv[nxt][j] = (ABL & 4) ? bv[cur][j] * 0.5f : Bs[kr * PT + j * 32];
+                    for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bv[cur][j]));
                 }
-                if (ks2 < RW && more) dma_b_row(c + 1, buf ^ 1, ks2);
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
-                if (ks2 + 1 < KC / 2) {
-                    // keep the next step's LDS reads ahead of this step's MFMAs
-                    __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
-                }
             }
             if constexpr ((ABL & 8) == 0) __syncthreads();  // next stage landed everywhere; this stage free
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -231,7 +231,15 @@ struct TileChoice {
 // pays for the partial slabs of tiles it splits plus one fixup launch.
 TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK) {
     static const int cfg[4][3] = {{128, 128, 2}, {128, 64, 3}, {64, 128, 3}, {64, 64, 4}};  // mt, pt, WG/CU
-    static const double ovh[4] = {1.0, 1.10, 1.10, 1.30};  // load/issue overhead per MFMA
+    // relative cost per MFMA of the smaller tiles (more load/issue work per MFMA); measured
+    // with scripts/conv_timing.py, overridable for A/B runs: OPOSE_TILE_OVH="1,1.02,1.02,1.06"
+    static double ovh[4] = {1.0, 1.02, 1.02, 1.06};
+    static const bool ovh_env = [] {
+        if (const char* e = getenv("OPOSE_TILE_OVH"))
+            std::sscanf(e, "%lf,%lf,%lf,%lf", &ovh[0], &ovh[1], &ovh[2], &ovh[3]);
+        return true;
+    }();
+    (void)ovh_env;
     TileChoice best{64, 64, 1};
     double best_cost = 1e300;
     for (int c = 0; c < 4; ++c) {
