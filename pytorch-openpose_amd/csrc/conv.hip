@@ -20,6 +20,8 @@
 //   order (deterministic), fusing bias + ReLU there.
 // * epilogue fuses bias + ReLU and writes into a channel slice of a wider buffer, so the
 //   reference's torch.cat([L1, L2, trunk]) (src/model.py:112-128) never materialises.
+#include <stdexcept>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -30,24 +32,34 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));  // native vector (HIP'
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-constexpr int KC = 32;   // k rows per chunk
-constexpr int NT = 256;  // threads per workgroup
+constexpr int KC = 32;  // k rows per chunk
+// waves per workgroup: 2 (M) x 2 (P) for tiles up to 128x128; 8 waves of 64x64 for the
+// 128x256 / 256x128 tiles (one workgroup per CU: each 32-k weight tile in LDS feeds twice the
+// MFMAs, or each gathered im2col row does)
+constexpr int wg_waves(int mt, int pt) { return mt * pt >= 32768 ? 8 : 4; }
 
-// TAP: K ordered (tap, channel) with Cin padded to a multiple of KC -> one bounds check per
-// pixel per chunk and a wave-uniform channel stride (all layers with Cin >= 32); otherwise K is
+// TAP: K ordered (channel block of KC, tap, channel) with Cin padded to a multiple of KC -> one
+// bounds check per pixel per chunk, a wave-uniform channel stride, and all taps of a channel
+// block back to back, so a workgroup re-reads its shifted im2col rows from L2 (and L1) while
+// they are resident (tap-outer order re-touched each channel after a full sweep of all
+// channels -- 4 MB of live gathers per XCD, which thrashed L2).  Layers with Cin >= 32; else K is
 // the OIHW flattening decoded through `ktab` (conv1_1: K = 27).
 // KS: compile-time kernel size (1, 3, 7) so the tap decode folds; 0 = runtime a.ks.
 // ABL: timing-only ablations (never launched in production): 1 skip the im2col gather,
-// 2 skip the weight load, 4 skip the LDS fragment reads, 8 skip the per-chunk barrier.
+// 2 skip the weight load, 4 skip the LDS fragment reads, 8 skip the per-chunk barrier,
+// 16 gather from cache-hot addresses (same rows every chunk), 32 cache-hot weight rows,
+// 128 barrier without waiting for the stage's DMA (wrong results; latency probe).
 template <int MT, int PT, bool TAP, int KS, int ABL = 0>
-__global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* __restrict__ ktab) {
+__global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void conv_igemm_f32(
+    ConvArgs a, const int* __restrict__ ktab) {
     const int ks = KS ? KS : a.ks;
-    constexpr int WM = MT / 2, WP = PT / 2;
+    constexpr int NW = wg_waves(MT, PT), NWM = NW == 8 ? MT / 64 : 2, NWP = NW / NWM;
+    constexpr int WM = MT / NWM, WP = PT / NWP;
     constexpr int TM = WM / 32, TN = WP / 32;
     constexpr int PJ = PT / 64;             // pixel columns per lane
-    constexpr int RW = KC / 4;              // k rows gathered per wave per chunk
+    constexpr int RW = KC / NW;             // k rows gathered per wave per chunk
     constexpr int A_SZ = KC * MT, B_SZ = KC * PT;
-    constexpr int A_PW = A_SZ / 256 / 4;    // 1-KiB A pieces per wave per chunk
+    constexpr int A_PW = A_SZ / 256 / NW;   // 1-KiB A pieces per wave per chunk
 
     // [2 stages][A tile KC x MT | B tile KC x PT] + bias; both tiles are filled by LDS-DMA
     // (buffer/global_load ... lds): no register staging, no ds_write pass.
@@ -62,8 +74,8 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
     const int HW = a.H * a.W;
     const uint32_t HW4 = (uint32_t)HW * 4u;
     float* s_bias = lds + 2 * (A_SZ + B_SZ);
-    const int wm0 = (wave & 1) * WM;
-    const int wp0 = (wave >> 1) * WP;
+    const int wm0 = (wave % NWM) * WM;
+    const int wp0 = (wave / NWM) * WP;
 
     // Stream-K: the (tile, k-chunk) iteration space is cut into gridDim.x equal contiguous
     // ranges, one per workgroup, so every CU gets the same work whatever the tile count
@@ -129,9 +141,10 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
 
         auto chunk_setup = [&](int c) __attribute__((always_inline)) {
             if constexpr (TAP) {
-                const int cpt = a.Kpad / (KC * ks * ks);  // chunks per tap (wave-uniform scalars)
-                const int tap = c / cpt;
-                ch0 = (c - tap * cpt) * KC + wave * RW;
+                const int taps = ks * ks;  // chunk c = (channel block, tap): wave-uniform scalars
+                const int cb = c / taps;
+                const int tap = c - cb * taps;
+                ch0 = cb * KC + wave * RW;
                 const int ky = tap / ks;
                 const int dy = ky - a.pad, dx = tap - ky * ks - a.pad;
                 const int shift = dy * a.W + dx;
@@ -153,8 +166,9 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
                 const uint32_t choff = (uint32_t)ch * HW4;
 #pragma unroll
                 for (int j = 0; j < PJ; ++j)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + j * 64), 4, base[j] + choff, 0, 0,
-                                                            0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        rsrc, (lds_ptr_t)(Bs + j * 64), 4,
+                        (ABL & 16) ? poff[j] * 4u + (uint32_t)r * HW4 : base[j] + choff, 0, 0, 0);
             } else {
                 const int code = ktab[c * KC + wave * RW + r];  // (c << 8) | (ky << 4) | kx
                 const int cch = code >> 8;
@@ -172,7 +186,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
         };
         auto dma_a = [&](int c, int buf) __attribute__((always_inline)) {
             if constexpr ((ABL & 2) != 0) return;
-            const int k0 = c * KC;
+            const int k0 = (ABL & 32) ? 0 : c * KC;
             float* As = lds + buf * (A_SZ + B_SZ);
 #pragma unroll
             for (int i = 0; i < A_PW; ++i) {
@@ -245,7 +259,8 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_f32(ConvArgs a, const int* _
                     for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
             }
-            if constexpr ((ABL & 8) == 0) __syncthreads();  // next stage landed everywhere; this stage free
+            if constexpr ((ABL & 128) != 0) asm volatile("s_barrier" ::: "memory");  // no DMA wait (timing only)
+            else if constexpr ((ABL & 8) == 0) __syncthreads();  // next stage landed everywhere; this stage free
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
 
@@ -368,16 +383,17 @@ __global__ __launch_bounds__(256) void maxpool2x2(const float* __restrict__ in, 
 template <int MT, int PT>
 static void launch_tile(const ConvArgs& a, const int* ktab, hipStream_t st) {
     const dim3 grid(a.sk_grid);
+    constexpr int NTH = 64 * wg_waves(MT, PT);
     if (!a.tap_major)
-        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, false, 0>), grid, dim3(NT), 0, st, a, ktab);
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, false, 0>), grid, dim3(NTH), 0, st, a, ktab);
     else if (a.ks == 7)
-        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 7>), grid, dim3(NT), 0, st, a, ktab);
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 7>), grid, dim3(NTH), 0, st, a, ktab);
     else if (a.ks == 3)
-        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 3>), grid, dim3(NT), 0, st, a, ktab);
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 3>), grid, dim3(NTH), 0, st, a, ktab);
     else if (a.ks == 1)
-        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 1>), grid, dim3(NT), 0, st, a, ktab);
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 1>), grid, dim3(NTH), 0, st, a, ktab);
     else
-        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 0>), grid, dim3(NT), 0, st, a, ktab);
+        hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 0>), grid, dim3(NTH), 0, st, a, ktab);
     const int tiles = (a.Mpad / MT) * ((a.npix + PT - 1) / PT) * a.ngroups;
     if (a.sk_grid != tiles)
         hipLaunchKernelGGL((conv_sk_fixup<MT, PT>), dim3(tiles, MT * PT / 1024), dim3(256), 0, st, a);
@@ -386,20 +402,27 @@ static void launch_tile(const ConvArgs& a, const int* ktab, hipStream_t st) {
 void launch_conv_ablation(const ConvArgs& a, int ablate, hipStream_t st) {
     const dim3 grid(a.sk_grid);
     switch (ablate) {
-        case 3: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 3>), grid, dim3(NT), 0, st, a, nullptr); break;
-        case 7: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 7>), grid, dim3(NT), 0, st, a, nullptr); break;
-        case 11: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 11>), grid, dim3(NT), 0, st, a, nullptr); break;
-        case 15: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 15>), grid, dim3(NT), 0, st, a, nullptr); break;
-        case 1: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 1>), grid, dim3(NT), 0, st, a, nullptr); break;
-        default: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 2>), grid, dim3(NT), 0, st, a, nullptr); break;
+        case 3: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 3>), grid, dim3(256), 0, st, a, nullptr); break;
+        case 7: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 7>), grid, dim3(256), 0, st, a, nullptr); break;
+        case 11: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 11>), grid, dim3(256), 0, st, a, nullptr); break;
+        case 15: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 15>), grid, dim3(256), 0, st, a, nullptr); break;
+        case 1: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 1>), grid, dim3(256), 0, st, a, nullptr); break;
+        case 16: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 16>), grid, dim3(256), 0, st, a, nullptr); break;
+        case 32: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 32>), grid, dim3(256), 0, st, a, nullptr); break;
+        case 48: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 48>), grid, dim3(256), 0, st, a, nullptr); break;
+        case 128: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 128>), grid, dim3(256), 0, st, a, nullptr); break;
+        default: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 2>), grid, dim3(256), 0, st, a, nullptr); break;
     }
 }
 
 void launch_conv(const ConvArgs& a, const int* ktab, int mt, int pt, hipStream_t st) {
     if (mt == 128 && pt == 128) launch_tile<128, 128>(a, ktab, st);
+    else if (mt == 128 && pt == 256) launch_tile<128, 256>(a, ktab, st);
+    else if (mt == 256 && pt == 128) launch_tile<256, 128>(a, ktab, st);
     else if (mt == 128 && pt == 64) launch_tile<128, 64>(a, ktab, st);
     else if (mt == 64 && pt == 128) launch_tile<64, 128>(a, ktab, st);
-    else launch_tile<64, 64>(a, ktab, st);
+    else if (mt == 64 && pt == 64) launch_tile<64, 64>(a, ktab, st);
+    else throw std::invalid_argument("unsupported conv tile");
 }
 
 void launch_maxpool(const float* in, float* out, int NC, int H, int W, hipStream_t st) {

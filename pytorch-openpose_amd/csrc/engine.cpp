@@ -119,7 +119,7 @@ struct DevBuf {
 struct DevConv {
     std::string name;
     int cin = 0, cout = 0, ks = 0, pad = 0, K = 0, Kpad = 0, Mpad = 0;
-    bool tap_major = false;  // K = (tap, channel padded to 32); see conv.hip
+    bool tap_major = false;  // K = (channel block of 32, tap, channel); see conv.hip
     float* wt = nullptr;
     float* bias = nullptr;
     int* ktab = nullptr;
@@ -230,26 +230,30 @@ struct TileChoice {
 // SIMD) runs at ~60 %.  Stream-K (grid = all resident slots) balances the chip exactly and
 // pays for the partial slabs of tiles it splits plus one fixup launch.
 TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK) {
-    static const int cfg[4][3] = {{128, 128, 2}, {128, 64, 3}, {64, 128, 3}, {64, 64, 4}};  // mt, pt, WG/CU
+    static const int cfg[6][3] = {{128, 128, 2}, {128, 256, 1}, {256, 128, 1},
+                                  {128, 64, 3},  {64, 128, 3},  {64, 64, 4}};  // mt, pt, WG/CU
     // relative cost per MFMA of the smaller tiles (more load/issue work per MFMA); measured
-    // with scripts/conv_timing.py, overridable for A/B runs: OPOSE_TILE_OVH="1,1.02,1.02,1.06"
-    static double ovh[4] = {1.0, 1.02, 1.02, 1.06};
+    // with scripts/conv_timing.py, overridable for A/B runs: OPOSE_TILE_OVH="1,.95,.93,1.02,1.02,1.06"
+    static double ovh[6] = {1.0, 0.95, 0.93, 1.02, 1.02, 1.06};
     static const bool ovh_env = [] {
         if (const char* e = getenv("OPOSE_TILE_OVH"))
-            std::sscanf(e, "%lf,%lf,%lf,%lf", &ovh[0], &ovh[1], &ovh[2], &ovh[3]);
+            std::sscanf(e, "%lf,%lf,%lf,%lf,%lf,%lf", &ovh[0], &ovh[1], &ovh[2], &ovh[3], &ovh[4], &ovh[5]);
         return true;
     }();
     (void)ovh_env;
     TileChoice best{64, 64, 1};
     double best_cost = 1e300;
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < 6; ++c) {
         const int mt = cfg[c][0], pt = cfg[c][1], occ = cfg[c][2];
         if (Mpad % mt) continue;
         const long tiles = (long)(Mpad / mt) * ((npix + pt - 1) / pt) * ngroups;
         const double unit = (mt / 64.0) * (pt / 64.0) * ovh[c];
         // data parallel
         const long per_cu = (tiles + 255) / 256;
-        const double dp = std::max<double>(per_cu, 1.6) * nK * unit;
+        // one resident workgroup of a 2-per-CU config runs at ~60 % (floor 1.6); the 8-wave
+        // 128x256 config fills the CU on its own
+        const double floor1 = occ >= 2 ? 1.6 : 1.0;
+        const double dp = std::max<double>(per_cu, floor1) * nK * unit;
         if (dp < best_cost * 0.97) {
             best_cost = dp;
             best = {mt, pt, (int)tiles};
@@ -259,7 +263,7 @@ TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK) {
         long grid = std::min<long>(256L * occ, iters / 4);
         if (grid >= 1 && grid != tiles) {
             const double per_wg = (double)iters / grid;
-            const double cu_load = std::max(1.6, std::ceil(grid / 256.0)) * per_wg * unit;
+            const double cu_load = std::max(floor1, std::ceil(grid / 256.0)) * per_wg * unit;
             const long split = std::min<long>(tiles, 2 * grid);                 // tiles with partials
             const double slab_bytes = (double)split * mt * pt * 4.0 * 3.0;       // write + re-read + out
             const double sk = cu_load + slab_bytes / 5e12 / 0.42e-6 + 8.0;      // + fixup launch
@@ -306,7 +310,10 @@ static void upload_conv(opose_ctx* h, int net, const std::string& key, const std
             for (int k = 0; k < dc->K; ++k) {
                 // reference layout OIHW: k = c * ks*ks + tap
                 const int c = k / (s0.ks * s0.ks), tap = k % (s0.ks * s0.ks);
-                const int kk = dc->tap_major ? tap * cin_pad + c : k;
+                // blocked layout: K = (32-channel block, tap, channel in block) -- a workgroup
+                // walks all taps of one channel block before the next, so the im2col rows it
+                // gathers are re-read from L2 while still resident (see conv.hip)
+                const int kk = dc->tap_major ? ((c / 32) * (s0.ks * s0.ks) + tap) * 32 + (c % 32) : k;
                 wt[(size_t)kk * dc->Mpad + m0 + m] = w[i][(size_t)m * dc->K + k];
             }
             bias[m0 + m] = b[i][m];

@@ -15,7 +15,9 @@ cases = [  # name, N, Cin, H, W, Cout, ks, ngroups
     ("conv1_2", 32, 64, 184, 328, 64, 3, 1),
     ("Mconv2 1 frame", 1, 128, 23, 41, 128, 7, 2),
 ]
-variants = [(0, 0, 0, 0), (128, 128, 0, 0), (128, 128, 512, 0), (128, 128, 0, 3), (128, 128, 512, 3),
+variants = [(0, 0, 0, 0), (128, 128, 0, 0), (128, 128, 512, 0), (128, 256, 0, 0), (128, 256, 256, 0),
+            (256, 128, 0, 0), (256, 128, 256, 0),
+            (128, 128, 0, 3), (128, 128, 512, 3),
             (64, 128, 0, 0), (128, 64, 0, 0), (64, 64, 0, 0)]
 only = sys.argv[1:] or None
 for name, N, Cin, H, W, Cout, ks, ng in cases:

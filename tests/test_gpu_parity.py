@@ -68,10 +68,22 @@ def test_conv_heuristic_tiles(native, handle, N, Cin, H, W, Cout, ks):
     _conv_case(native, handle, N, Cin, H, W, Cout, ks, relu=True)
 
 
-@pytest.mark.parametrize("mt,pt,splits", [(128, 128, 1), (128, 64, 1), (64, 128, 1), (64, 64, 1),
-                                          (128, 128, 4), (64, 64, 7), (128, 64, 3)])
+@pytest.mark.parametrize("mt,pt,splits", [(128, 128, 1), (128, 64, 1), (64, 128, 1), (64, 64, 1), (128, 256, 1),
+                                          (128, 128, 4), (64, 64, 7), (128, 64, 3), (128, 256, 5), (128, 256, 0)])
 def test_conv_every_tile_and_split(native, handle, mt, pt, splits):
     _conv_case(native, handle, 2, 96, 17, 29, 128, 3, relu=False, mt=mt, pt=pt, splits=splits, seed=3)
+
+
+@pytest.mark.parametrize("cout,mt,pt,splits", [(128, 128, 256, 0), (128, 128, 256, 7), (128, 128, 128, 9),
+                                               (256, 256, 128, 0), (256, 256, 128, 5), (192, 256, 128, 3)])
+def test_conv_7x7_tiles(native, handle, cout, mt, pt, splits):
+    # Mconv shapes (128 -> 128 / 256, 7x7) on a ragged pixel count
+    _conv_case(native, handle, 3, 128, 23, 41, cout, 7, relu=True, mt=mt, pt=pt, splits=splits, seed=4)
+
+
+@pytest.mark.parametrize("splits", [0, 1, 6])
+def test_conv_256_rows(native, handle, splits):
+    _conv_case(native, handle, 2, 96, 17, 29, 256, 3, relu=False, mt=256, pt=128, splits=splits, seed=5)
 
 
 def test_preprocess_bit_exact(native, handle):
