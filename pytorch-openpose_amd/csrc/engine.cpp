@@ -570,7 +570,8 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
         const bool f32 = ns == 1;
         double* avg = h->avg.ensure<double>((size_t)N * 18 * H * W, h->stream);
         for (int s = 0; s < ns; ++s) {
-            h->prof_begin(pe, "heat_full", 0, (double)N * 18 * H * W * (f32 ? 4 : 8) * (s ? 2 : 1));
+            h->prof_begin(pe, "heat_full", 0,
+                          (double)N * 18 * (H * W * (f32 ? 4.0 : 8.0) * (s ? 2 : 1) + 4.0 * gs[s].Hs * gs[s].Ws));
             if (f32)
                 launch_heat_full_f32(S.mid[s], 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx,
                                      reinterpret_cast<float*>(avg), h->stream);

@@ -5,7 +5,7 @@
 //                       util.padRightDownCorner (src/util.py:12-32), float32(x)/256 - 0.5,
 //                       HWC -> NCHW                       => preprocess_u8
 //  * src/body.py:55-56  cv2.resize(map, fx=fy=8, INTER_CUBIC) + crop of the padding
-//                                                         => upsample8  (writes only the crop)
+//                                                         => cubic_resize_rows<0> (writes only the crop)
 //  * src/body.py:57,67  cv2.resize(map, (W, H)) + heatmap_avg += map / n_scales (float64)
 //                                                         => heat_full_accum
 // Compiled with -ffp-contract=off (see cubic.h).
@@ -65,21 +65,6 @@ __global__ __launch_bounds__(256) void preprocess_u8(const uint8_t* __restrict__
     }
 }
 
-// x8 cubic upsample of the low-res network maps, cropped to Hs x Ws (float32).
-// in: [N][in_cstride][hl][wl] channels [in_coff, in_coff + C); out: [N][C][Hs][Ws]
-__global__ __launch_bounds__(256) void upsample8(const float* __restrict__ in, int in_cstride, int in_coff, int C,
-                                                 int hl, int wl, int Hs, int Ws, float* __restrict__ out) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    const int nc = blockIdx.z;
-    if (x >= Ws) return;
-    const int n = nc / C, c = nc - n * C;
-    const CubicTap ty = cubic_tap(y, 0.125, hl);
-    const CubicTap tx = cubic_tap(x, 0.125, wl);
-    const float* plane = in + ((size_t)n * in_cstride + in_coff + c) * hl * wl;
-    out[((size_t)nc * Hs + y) * Ws + x] = cubic_sample_f32(plane, wl, ty, tx);
-}
-
 // cubic resize of mid [N][Cm][Hs][Ws] channels [coff, coff+P) to [H][W], then
 // avg[n][p] (+)= (double)(v / nscales)   (float32 divide, float64 accumulate).
 // T = float when there is a single scale: the average is then exactly the float32 resize
@@ -103,6 +88,85 @@ __global__ __launch_bounds__(256) void heat_full_accum(const float* __restrict__
     else *d = accumulate ? *d + (double)v : 0.0 + (double)v;
 }
 
+// Row-staged cubic resize (the fast path of upsample8 / heat_full_accum, same arithmetic):
+// a workgroup owns RT output rows x 256 output columns of one plane.  OpenCV's horizontal pass
+// h[r][x] = ((p0*a0 + p1*a1) + p2*a2) + p3*a3 is computed once per (source row, output column)
+// into LDS, then every output row combines its 4 staged rows vertically -- instead of
+// recomputing 4 horizontal sums (16 scattered loads) per output pixel.  Bit-identical to
+// cubic_sample_f32: the same expressions in the same order.
+// MODE 0: out[nc] = v (x8 upsample into mid), 1: float heat map 0.f + v/ns,
+// 2: float64 heat average (+)= (double)(v/ns).
+constexpr int RS_RT = 16;      // output rows per workgroup
+constexpr int RS_MAXR = 44;    // staged source rows (RT * scale + 5 <= 44  <=>  scale <= 2.4)
+
+// MAXR: LDS rows actually staged (8 for x8, 16 for x2): small tiles keep many workgroups
+// resident, which this HBM-bound kernel needs
+template <int MODE, int MAXR>
+__global__ __launch_bounds__(256) void cubic_resize_rows(const float* __restrict__ in, int in_cstride, int in_coff,
+                                                         int C, int hi, int wi, int ho, int wo, double sy, double sx,
+                                                         float nscales, int accumulate, void* __restrict__ out) {
+    __shared__ float hs[MAXR][256];
+    const int tid = threadIdx.x;
+    const int x = blockIdx.x * 256 + tid;
+    const int y0 = blockIdx.y * RS_RT;
+    const int y1 = min(y0 + RS_RT, ho);
+    const int nc = blockIdx.z;
+    const int n = nc / C, c = nc - n * C;
+    const float* plane = in + ((size_t)n * in_cstride + in_coff + c) * hi * wi;
+    // staged source rows: the clamped tap rows of the first and last output row bound them
+    const int r_lo = cubic_tap(y0, sy, hi).i[0];
+    const int r_hi = cubic_tap(y1 - 1, sy, hi).i[3];
+    const bool live = x < wo;
+    if (live) {
+        const CubicTap tx = cubic_tap(x, sx, wi);
+        for (int r = r_lo; r <= r_hi; ++r) {
+            const float* row = plane + (size_t)r * wi;
+            float v = row[tx.i[0]] * tx.c[0];
+            v = v + row[tx.i[1]] * tx.c[1];
+            v = v + row[tx.i[2]] * tx.c[2];
+            v = v + row[tx.i[3]] * tx.c[3];
+            hs[r - r_lo][tid] = v;
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    for (int y = y0; y < y1; ++y) {
+        const CubicTap ty = cubic_tap(y, sy, hi);
+        float o = hs[ty.i[0] - r_lo][tid] * ty.c[0];
+        o = o + hs[ty.i[1] - r_lo][tid] * ty.c[1];
+        o = o + hs[ty.i[2] - r_lo][tid] * ty.c[2];
+        o = o + hs[ty.i[3] - r_lo][tid] * ty.c[3];
+        const size_t e = ((size_t)nc * ho + y) * wo + x;
+        if constexpr (MODE == 0) {
+            reinterpret_cast<float*>(out)[e] = o;
+        } else if constexpr (MODE == 1) {
+            reinterpret_cast<float*>(out)[e] = 0.f + o / nscales;
+        } else {
+            double* d = reinterpret_cast<double*>(out) + e;
+            const float v = o / nscales;
+            *d = accumulate ? *d + (double)v : 0.0 + (double)v;
+        }
+    }
+}
+
+// staged rows needed by one workgroup for a source step `scale` (destination -> source)
+static bool rows_fit(double scale) { return RS_RT * scale + 5.0 <= (double)RS_MAXR; }
+
+template <int MODE>
+static void launch_resize_rows(dim3 grid, hipStream_t st, const float* in, int cstride, int coff, int C, int hi,
+                               int wi, int ho, int wo, double sy, double sx, float ns, int acc, void* out) {
+    const double need = RS_RT * sy + 5.0;
+    if (need <= 8.0)
+        hipLaunchKernelGGL((cubic_resize_rows<MODE, 8>), grid, dim3(256), 0, st, in, cstride, coff, C, hi, wi, ho, wo,
+                           sy, sx, ns, acc, out);
+    else if (need <= 16.0)
+        hipLaunchKernelGGL((cubic_resize_rows<MODE, 16>), grid, dim3(256), 0, st, in, cstride, coff, C, hi, wi, ho,
+                           wo, sy, sx, ns, acc, out);
+    else
+        hipLaunchKernelGGL((cubic_resize_rows<MODE, RS_MAXR>), grid, dim3(256), 0, st, in, cstride, coff, C, hi, wi,
+                           ho, wo, sy, sx, ns, acc, out);
+}
+
 void launch_preprocess(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int Hs,
                        int Ws, double sy, double sx, int Hp, int Wp, float pad_val, float* out, hipStream_t st) {
     dim3 grid((Wp + 255) / 256, Hp, N);
@@ -112,12 +176,17 @@ void launch_preprocess(const uint8_t* src, int64_t frame_stride, int64_t row_str
 
 void launch_upsample8(const float* in, int in_cstride, int in_coff, int C, int N, int hl, int wl, int Hs, int Ws,
                       float* out, hipStream_t st) {
-    dim3 grid((Ws + 255) / 256, Hs, N * C);
-    hipLaunchKernelGGL(upsample8, grid, dim3(256), 0, st, in, in_cstride, in_coff, C, hl, wl, Hs, Ws, out);
+    dim3 grid((Ws + 255) / 256, (Hs + RS_RT - 1) / RS_RT, N * C);
+    launch_resize_rows<0>(grid, st, in, in_cstride, in_coff, C, hl, wl, Hs, Ws, 0.125, 0.125, 1.f, 0, (void*)out);
 }
 
 void launch_heat_full(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
                       double sx, int nscales, int accumulate, double* avg, hipStream_t st) {
+    if (!(Hs == H && Ws == W) && rows_fit(sy)) {
+        dim3 grid((W + 255) / 256, (H + RS_RT - 1) / RS_RT, N * P);
+        launch_resize_rows<2>(grid, st, mid, Cm, coff, P, Hs, Ws, H, W, sy, sx, (float)nscales, accumulate, (void*)avg);
+        return;
+    }
     dim3 grid((W + 255) / 256, H, N * P);
     hipLaunchKernelGGL(heat_full_accum<double>, grid, dim3(256), 0, st, mid, Cm, coff, P, Hs, Ws, H, W, sy, sx,
                        (float)nscales, accumulate, avg);
@@ -125,6 +194,11 @@ void launch_heat_full(const float* mid, int Cm, int coff, int P, int N, int Hs, 
 
 void launch_heat_full_f32(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
                           double sx, float* avg, hipStream_t st) {
+    if (!(Hs == H && Ws == W) && rows_fit(sy)) {
+        dim3 grid((W + 255) / 256, (H + RS_RT - 1) / RS_RT, N * P);
+        launch_resize_rows<1>(grid, st, mid, Cm, coff, P, Hs, Ws, H, W, sy, sx, 1.f, 0, (void*)avg);
+        return;
+    }
     dim3 grid((W + 255) / 256, H, N * P);
     hipLaunchKernelGGL(heat_full_accum<float>, grid, dim3(256), 0, st, mid, Cm, coff, P, Hs, Ws, H, W, sy, sx, 1.f, 0,
                        avg);
