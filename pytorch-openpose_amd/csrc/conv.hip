@@ -6,18 +6,18 @@
 //
 // GEMM view of a stride-1 'same' convolution over a batch of NCHW frames:
 //   out[m][p] = bias[m] + sum_k  W[m][k] * im2col[k][p]
-//   m = output channel, p = (frame, y, x) flattened, k = (c, ky, kx) in OIHW order.
-// * A = weights, pre-transposed once at load time to Wt[Kpad][Mpad] (zero padded), so a
-//   KC x MT tile is MT contiguous floats per k row (16-B vector loads, ds_write_b128).
-// * B = im2col gathered on the fly from the NCHW activation (L2-resident at these sizes):
-//   every wave loads whole k rows for 64 consecutive pixels -> coalesced along x; the
-//   k -> (c, ky, kx) decode is wave-uniform (scalar loads of a per-layer table).
-// * v_mfma_f32_32x32x2_f32: exact fp32 (bitwise an fmaf chain), 64 FLOP/clk/SIMD.  A
-//   256-thread workgroup = 2x2 waves, each wave owns (MT/2)x(PT/2) outputs =
-//   (MT/64)x(PT/64) 32x32 accumulators; K is consumed in chunks of 32 through a
-//   double-buffered LDS tile with register staging (one barrier per chunk).
-// * split-K (gridDim.z) writes fp32 partial slabs that a second kernel sums in a fixed
-//   order (deterministic), fusing bias + ReLU there.
+//   m = output channel, p = (frame, y, x) flattened, k = (channel block, tap, channel).
+// * A = weights, pre-transposed once at load time to Wt[Kpad][Mpad] (zero padded); a KC x MT
+//   tile is KC rows of MT contiguous floats, copied to LDS by global_load_lds_dwordx4.
+// * B = im2col gathered on the fly from the NCHW activation by buffer_load_dword ... lds:
+//   every DMA covers one k row for 64 consecutive pixels (coalesced along x); zero padding
+//   comes from the buffer range check (no branches, no register staging).
+// * v_mfma_f32_32x32x2_f32: exact fp32 (bitwise an fmaf chain), 64 FLOP/clk/SIMD.  4 waves
+//   (2x2) per workgroup for tiles up to 128x128, 8 waves of 64x64 for 128x256 / 256x128;
+//   K is consumed in chunks of 32 through a double-buffered LDS tile (one barrier per chunk).
+// * stream-K: the (tile, k-chunk) space is split evenly over the grid; tiles shared by
+//   several workgroups leave fp32 partial slabs that conv_sk_fixup sums in k order
+//   (deterministic), fusing bias + ReLU there.
 // * epilogue fuses bias + ReLU and writes into a channel slice of a wider buffer, so the
 //   reference's torch.cat([L1, L2, trunk]) (src/model.py:112-128) never materialises.
 #include <stdexcept>
