@@ -46,6 +46,8 @@ struct ConvArgs {
     int ngroups;        // 1 or 2 GEMM groups sharing the launch
     int sk_grid;        // stream-K workgroups (== tiles: plain data-parallel grid)
     float* partial;     // stream-K partial slabs [2 * sk_grid][MT * PT]
+    int* sk_cnt;        // per-tile arrival counters (zero between launches) -> the last
+                        // workgroup of a split tile reduces it; nullptr: conv_sk_fixup launch
 };
 
 // ---------------------------------------------------------------- body records

@@ -49,6 +49,53 @@ constexpr int wg_waves(int mt, int pt) { return mt * pt >= 32768 ? 8 : 4; }
 // 2 skip the weight load, 4 skip the LDS fragment reads, 8 skip the per-chunk barrier,
 // 16 gather from cache-hot addresses (same rows every chunk), 32 cache-hot weight rows,
 // 128 barrier without waiting for the stage's DMA (wrong results; latency probe).
+// device-coherent 16-byte load (sc1: served from the coherence point, not a possibly stale
+// line in this XCD's L2) -- reads partial slabs written by other workgroups in this launch
+__device__ __forceinline__ f32x4 load_sc1(const float* p) {
+    f32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
+// Sum the partial slabs of `tile` (workgroups w0..w1, k order) + bias + ReLU -> channel slice.
+// Called by the last workgroup to finish a part of the tile; mirrors conv_sk_fixup.
+template <int MT, int PT, int NTH>
+__device__ __forceinline__ void reduce_tile(const ConvArgs& a, const ConvGroup& G, int tile, int m0, int p0, int w0,
+                                            int w1, int nK, long long I, int Gw, const float* s_bias, int HW) {
+    for (int e = threadIdx.x * 4; e < MT * PT; e += NTH * 4) {
+        const int ml = e / PT, pl = e - ml * PT;
+        const int m = m0 + ml;
+        if (m >= G.cout) continue;
+        f32x4 v;
+        for (int w = w0; w <= w1; w += 4) {  // 4 loads in flight, summed in k order
+            f32x4 part[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int ww = min(w + u, w1);
+                const long long lo_w = (long long)ww * I / Gw;
+                const int slot = (lo_w / nK == tile) ? 2 * ww : 2 * ww + 1;
+                part[u] = load_sc1(a.partial + (size_t)slot * (MT * PT) + e);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(part[0]), "+v"(part[1]), "+v"(part[2]), "+v"(part[3]));
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (w + u <= w1) v = (w + u == w0) ? part[u] : v + part[u];
+        }
+        const float bias = s_bias[ml];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int p = p0 + pl + k;
+            if (p >= a.npix) break;
+            float o = v[k] + bias;
+            if (G.relu) o = fmaxf(o, 0.f);
+            const int n = p / HW;
+            const int rem = p - n * HW;
+            G.out[((size_t)n * G.out_cstride + G.out_coff + m) * HW + rem] = o;
+            if (G.out2) G.out2[((size_t)n * G.out2_cstride + G.out2_coff + m) * HW + rem] = o;
+        }
+    }
+}
+
 template <int MT, int PT, bool TAP, int KS, int ABL = 0>
 __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void conv_igemm_f32(
     ConvArgs a, const int* __restrict__ ktab) {
@@ -64,6 +111,7 @@ __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void c
     // [2 stages][A tile KC x MT | B tile KC x PT] + bias; both tiles are filled by LDS-DMA
     // (buffer/global_load ... lds): no register staging, no ds_write pass.
     __shared__ __attribute__((aligned(16))) float lds[2 * (A_SZ + B_SZ) + MT];
+    __shared__ int s_last;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -278,7 +326,11 @@ __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void c
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int ml = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-                        slab[ml * PT + pl] = acc[i][j][r];
+                        // sc1: device-scope store, written through to the coherence point so
+                        // the workgroup that reduces the tile (maybe on another XCD) sees it
+                        asm volatile("global_store_dword %0, %1, off sc1" ::"v"(slab + ml * PT + pl),
+                                     "v"(acc[i][j][r])
+                                     : "memory");
                     }
                 continue;
             }
@@ -299,6 +351,21 @@ __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void c
                         if (ob2) ob2[(size_t)m * HW] = v;
                     }
                 }
+        }
+        // ---- stream-K reduction: the last workgroup to finish a part of this tile sums all the
+        // parts in k order (deterministic, same order as conv_sk_fixup) + bias + ReLU.
+        if (!whole && a.sk_cnt) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab stores are acked
+            __syncthreads();
+            const long long x0 = (long long)tile * nK;
+            const int w0 = (int)(((x0 + 1) * Gw - 1) / I);   // workgroups holding the tile's
+            const int w1 = (int)(((x0 + nK) * Gw - 1) / I);  // first / last chunk
+            if (tid == 0) s_last = atomicAdd(a.sk_cnt + tile, 1) == w1 - w0;
+            __syncthreads();
+            if (s_last) {
+                reduce_tile<MT, PT, 64 * NW>(a, G, tile, m0, p0, w0, w1, nK, I, Gw, s_bias, HW);
+                if (tid == 0) atomicExch(a.sk_cnt + tile, 0);  // ready for the next launch
+            }
         }
         first = 0;
     }
@@ -395,7 +462,7 @@ static void launch_tile(const ConvArgs& a, const int* ktab, hipStream_t st) {
     else
         hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 0>), grid, dim3(NTH), 0, st, a, ktab);
     const int tiles = (a.Mpad / MT) * ((a.npix + PT - 1) / PT) * a.ngroups;
-    if (a.sk_grid != tiles)
+    if (a.sk_grid != tiles && !a.sk_cnt)
         hipLaunchKernelGGL((conv_sk_fixup<MT, PT>), dim3(tiles, MT * PT / 1024), dim3(256), 0, st, a);
 }
 

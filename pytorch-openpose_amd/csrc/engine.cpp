@@ -156,7 +156,20 @@ struct opose_ctx {
     bool loaded[2] = {false, false};
     // workspace
     DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[kMaxScales], avg, cnt, list, peak_pos, part_cnt,
-        score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score;
+        score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score, skcnt;
+    // stream-K: split tiles reduced by the conv_sk_fixup launch (default) or in-kernel by the
+    // last arriving workgroup (OPOSE_SK_INKERNEL=1; measured 0.4 % slower at batch 32: the
+    // reducing workgroup's serial slab reads stall its next tile more than the launch costs)
+    bool sk_fixup_kernel = getenv("OPOSE_SK_INKERNEL") == nullptr;
+    // per-tile arrival counters for a stream-K launch; zero between launches (the reducing
+    // workgroup resets its tile), zero-filled whenever the buffer grows
+    int* sk_counters(int tiles) {
+        if (sk_fixup_kernel) return nullptr;
+        const size_t before = skcnt.bytes;
+        int* c = skcnt.ensure<int>((size_t)tiles, stream);
+        if (skcnt.bytes != before) OPOSE_HIP_CHECK(hipMemsetAsync(c, 0, skcnt.bytes, stream));
+        return c;
+    }
     // profiling
     bool prof = false;
     bool detail = false;  // per-layer aggregation (opose_profile_enable(h, 2))
@@ -382,6 +395,7 @@ static void run_conv(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W
     a.ngroups = ng;
     a.sk_grid = t.grid;
     a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+    a.sk_cnt = h->sk_counters((a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * ng);
     double flops = 0;
     for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)a.K * a.npix;
     ProfEntry pe;
@@ -1004,6 +1018,7 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
         a.ngroups = 1;
         a.sk_grid = t.grid;
         a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        a.sk_cnt = h->sk_counters((a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * a.ngroups);
         launch_conv(a, c->ktab, t.mt, t.pt, h->stream);
         OPOSE_HIP_CHECK(hipMemcpyAsync(out, yd, ny * 4, hipMemcpyDeviceToHost, h->stream));
         OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
@@ -1046,6 +1061,7 @@ int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, in
         a.ngroups = ngroups;
         a.sk_grid = t.grid;
         a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        a.sk_cnt = h->sk_counters((a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * a.ngroups);
         auto go = [&]() {
             if (ablate) {
                 if (!(a.tap_major && a.ks == 7 && t.mt == 128 && t.pt == 128))
