@@ -173,7 +173,6 @@ struct opose_ctx {
     // profiling
     bool prof = false;
     bool detail = false;  // per-layer aggregation (opose_profile_enable(h, 2))
-    bool fused_heat = getenv("OPOSE_FUSED_HEAT") != nullptr;  // A/B switch for the heat chain
     std::vector<ProfEntry> pending;
     std::map<std::string, ProfAgg> agg;
     std::vector<hipEvent_t> event_pool;
@@ -574,30 +573,23 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     int* ccnt = h->conn_cnt.ensure<int>((size_t)N * 19, h->stream);
     OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * N * 18, h->stream));
     ProfEntry pe;
-    if (h->fused_heat) {
-        // heat average (src/body.py:55-67) evaluated on the fly inside the Gaussian tiles
-        h->prof_begin(pe, "gauss_nms", 0, (double)N * 18 * 4.0 * gs[0].Hs * gs[0].Ws * ns);
-        launch_gauss_nms_fused(S, N, 38, p.thre1, cap, cnt, list, lscore, h->stream);
-        h->prof_end(pe);
-    } else {
-        // single scale: the float64 average equals the float32 resize output exactly -> f32 map
-        const bool f32 = ns == 1;
-        double* avg = h->avg.ensure<double>((size_t)N * 18 * H * W, h->stream);
-        for (int s = 0; s < ns; ++s) {
-            h->prof_begin(pe, "heat_full", 0,
-                          (double)N * 18 * (H * W * (f32 ? 4.0 : 8.0) * (s ? 2 : 1) + 4.0 * gs[s].Hs * gs[s].Ws));
-            if (f32)
-                launch_heat_full_f32(S.mid[s], 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx,
-                                     reinterpret_cast<float*>(avg), h->stream);
-            else
-                launch_heat_full(S.mid[s], 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx, ns,
-                                 s > 0, avg, h->stream);
-            h->prof_end(pe);
-        }
-        h->prof_begin(pe, "gauss_nms", 0, (double)N * 18 * H * W * (f32 ? 4 : 8));
-        launch_gauss_nms(avg, f32, N * 18, H, W, p.thre1, cap, cnt, list, lscore, h->stream);
+    // single scale: the float64 average equals the float32 resize output exactly -> f32 map
+    const bool f32 = ns == 1;
+    double* avg = h->avg.ensure<double>((size_t)N * 18 * H * W, h->stream);
+    for (int s = 0; s < ns; ++s) {
+        h->prof_begin(pe, "heat_full", 0,
+                      (double)N * 18 * (H * W * (f32 ? 4.0 : 8.0) * (s ? 2 : 1) + 4.0 * gs[s].Hs * gs[s].Ws));
+        if (f32)
+            launch_heat_full_f32(S.mid[s], 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx,
+                                 reinterpret_cast<float*>(avg), h->stream);
+        else
+            launch_heat_full(S.mid[s], 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx, ns, s > 0,
+                             avg, h->stream);
         h->prof_end(pe);
     }
+    h->prof_begin(pe, "gauss_nms", 0, (double)N * 18 * H * W * (f32 ? 4 : 8));
+    launch_gauss_nms(avg, f32, N * 18, H, W, p.thre1, cap, cnt, list, lscore, h->stream);
+    h->prof_end(pe);
     h->prof_begin(pe, "peaks_finalize", 0, 0);
     launch_peaks_finalize(cnt, list, lscore, N, H, W, L, rec_dev, pos, pcnt, h->stream);
     h->prof_end(pe);

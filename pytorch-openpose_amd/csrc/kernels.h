@@ -38,8 +38,6 @@ void launch_heat_full_f32(const float* mid, int Cm, int coff, int P, int N, int 
 // post.hip
 void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
                       double* list_score, hipStream_t st);
-void launch_gauss_nms_fused(const PafScales& S, int N, int ch0, double thre, int cap, int* cnt, int* list,
-                            double* list_score, hipStream_t st);
 void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st);
 void launch_peaks_finalize(const int* cnt, const int* list, const double* list_score, int N, int H, int W,
                            const RecordLayout& L, uint8_t* records, int* peak_pos, int* part_cnt, hipStream_t st);

@@ -36,49 +36,54 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
     return i < n ? i : p - 1 - i;
 }
 
-constexpr int GT = 32;        // output tile (GT x GT)
-constexpr int GI = GT + 26;   // input tile incl. 13-pixel halo on each side
-constexpr int GR = GT + 2;    // smoothed rows/cols incl. the NMS ring
+// Gaussian tile: TW x TH outputs of one map (+ the 1-pixel NMS ring).  scipy order: axis 0
+// (vertical) then axis 1, symmetric taps summed centre-first then |j| = 12 .. 1, float64, no FMA.
+//  * vertical pass straight from global memory: a thread owns one column of the tile's
+//    13-pixel-haloed footprint and half its rows, sliding a 41-entry register window down the
+//    column (one load per input, coalesced across threads), result -> LDS v[VR][VW];
+//  * horizontal pass: a thread owns one row and 10 columns of v, register window of 34;
+//  * NMS on the smoothed tile.
+// 64 x 32 outputs per tile: 2.6 filter evaluations per output pixel (halo included) instead
+// of 3.1 for 32 x 32 tiles, and no staged input tile (42 KB of LDS, 3 workgroups per CU).
+constexpr int TW = 64, TH = 32;
+constexpr int VW = TW + 26;   // vertical-pass columns: 13-pixel halo (12 filter + 1 ring) each side
+constexpr int VR = TH + 2;    // smoothed rows incl. the NMS ring
+constexpr int GW = TW + 2;    // smoothed cols incl. the NMS ring
+constexpr int VH = VR / 2;    // rows per thread in the vertical pass (two halves)
+constexpr int HC = 10;        // cols per thread in the horizontal pass (7 x 10 >= GW)
 
-// Smooth one GT x GT tile (plus a 1-pixel ring) of one map into s_g (scipy order: axis 0
-// then axis 1, symmetric taps summed centre-first then |j| = 12 .. 1, float64, no FMA).
 struct GaussTile {
-    double in[GI][GI];
-    double v[GR][GI];
-    double g[GR][GR];
+    double v[VR][VW];
+    double g[VR][GW];
 };
 
-constexpr int FR_V = 9;   // rows per thread in the vertical pass   (34 <= 4 x 9)
-constexpr int FR_H = 5;   // cols per thread in the horizontal pass (34 <= 7 x 5)
-
-// The two 25-tap passes over a loaded tile, each thread sliding a register window along a
-// column (axis 0) or row (axis 1): one LDS read per output instead of 25.
-__device__ __forceinline__ void gauss_passes(GaussTile& t) {
+template <typename T>
+__device__ __forceinline__ void gauss_tile(const T* __restrict__ m, int H, int W, int x0, int y0, GaussTile& t) {
     const int tid = threadIdx.x;
-    if (tid < 4 * GI) {  // axis 0: thread -> (column c, 9-row run)
-        const int c = tid % GI, r0 = (tid / GI) * FR_V;
-        double win[FR_V + 24];
+    if (tid < 2 * VW) {  // axis 0: thread -> (column c, half h)
+        const int c = tid % VW, h = tid / VW;
+        const T* col = m + reflect_idx(x0 - 13 + c, W);
+        const int r0 = y0 - 13 + h * VH;  // image row of window entry 0
+        double win[VH + 24];
 #pragma unroll
-        for (int i = 0; i < FR_V + 24; ++i) win[i] = (r0 + i < GI) ? t.in[r0 + i][c] : 0.0;
+        for (int i = 0; i < VH + 24; ++i) win[i] = (double)col[(size_t)reflect_idx(r0 + i, H) * W];
 #pragma unroll
-        for (int i = 0; i < FR_V; ++i) {
-            if (r0 + i < GR) {
-                double acc = win[i + 12] * kGauss[0];
+        for (int i = 0; i < VH; ++i) {
+            double acc = win[i + 12] * kGauss[0];
 #pragma unroll
-                for (int j = 12; j >= 1; --j) acc = acc + (win[i + 12 - j] + win[i + 12 + j]) * kGauss[j];
-                t.v[r0 + i][c] = acc;
-            }
+            for (int j = 12; j >= 1; --j) acc = acc + (win[i + 12 - j] + win[i + 12 + j]) * kGauss[j];
+            t.v[h * VH + i][c] = acc;
         }
     }
     __syncthreads();
-    if (tid < 7 * GR) {  // axis 1: thread -> (row r, 5-column run)
-        const int r = tid % GR, c0 = (tid / GR) * FR_H;
-        double win[FR_H + 24];
+    if (tid < VR * 7) {  // axis 1: thread -> (row r, 10-column run)
+        const int r = tid % VR, c0 = (tid / VR) * HC;
+        double win[HC + 24];
 #pragma unroll
-        for (int i = 0; i < FR_H + 24; ++i) win[i] = (c0 + i < GI) ? t.v[r][c0 + i] : 0.0;
+        for (int i = 0; i < HC + 24; ++i) win[i] = (c0 + i < VW) ? t.v[r][c0 + i] : 0.0;
 #pragma unroll
-        for (int i = 0; i < FR_H; ++i) {
-            if (c0 + i < GR) {
+        for (int i = 0; i < HC; ++i) {
+            if (c0 + i < GW) {
                 double acc = win[i + 12] * kGauss[0];
 #pragma unroll
                 for (int j = 12; j >= 1; --j) acc = acc + (win[i + 12 - j] + win[i + 12 + j]) * kGauss[j];
@@ -89,43 +94,32 @@ __device__ __forceinline__ void gauss_passes(GaussTile& t) {
     __syncthreads();
 }
 
-template <typename T>
-__device__ __forceinline__ void gauss_tile(const T* __restrict__ m, int H, int W, int x0, int y0, GaussTile& t) {
-    constexpr int IIT = (GI * GI + 255) / 256;
-    double iv[IIT];
-#pragma unroll
-    for (int it = 0; it < IIT; ++it) {  // all loads of a thread in flight together
-        const int e = min((int)threadIdx.x + it * 256, GI * GI - 1);
-        const int r = e / GI, c = e - r * GI;
-        iv[it] = (double)m[(size_t)reflect_idx(y0 - 13 + r, H) * W + reflect_idx(x0 - 13 + c, W)];
-    }
-#pragma unroll
-    for (int it = 0; it < IIT; ++it) {
-        const int e = threadIdx.x + it * 256;
-        if (e < GI * GI) t.in[e / GI][e % GI] = iv[it];
-    }
-    __syncthreads();
-    gauss_passes(t);
+// tile id -> (x tile, y tile, map) with an XCD-contiguous order (guide T1): horizontally and
+// vertically adjacent tiles, which re-read each other's 13-pixel halos, share an L2.
+__device__ __forceinline__ void gauss_tile_coords(int H, int W, int& x0, int& y0, int& np) {
+    const int ntx = (W + TW - 1) / TW, nty = (H + TH - 1) / TH;
+    const int total = gridDim.x, b = blockIdx.x;
+    const int q = total >> 3, rr = total & 7, xcd = b & 7;
+    const int id = xcd * q + min(xcd, rr) + (b >> 3);
+    const int tx = id % ntx, rest = id / ntx;
+    const int ty = rest % nty;
+    np = rest / nty;
+    x0 = tx * TW;
+    y0 = ty * TH;
 }
 
-// avg: [N*P][H][W] float64; one workgroup per GT x GT tile of one part of one frame.
-// 1-D grid over (x tile, y tile, map) with an XCD-contiguous order (guide T1): horizontally
-// and vertically adjacent tiles, which re-read each other's 13-pixel halos, share an L2.
+// avg: [N*P][H][W] (float32 single scale / float64 average); one workgroup per tile.
 template <typename T>
 __global__ __launch_bounds__(256) void gauss_nms(const T* __restrict__ avg, int P, int H, int W, double thre,
                                                  int cap, int* __restrict__ cnt, int* __restrict__ list,
                                                  double* __restrict__ list_score) {
     __shared__ GaussTile t;
-    const int ntx = (W + GT - 1) / GT, nty = (H + GT - 1) / GT;
-    const int total = gridDim.x, b = blockIdx.x;
-    const int q = total >> 3, rr = total & 7, xcd = b & 7;
-    const int id = xcd * q + min(xcd, rr) + (b >> 3);
-    const int tx = id % ntx, rest = id / ntx;
-    const int ty = rest % nty, np = rest / nty;
-    const int x0 = tx * GT, y0 = ty * GT;
-    gauss_tile(avg + (size_t)np * H * W, H, W, x0, y0, t);
-    for (int e = threadIdx.x; e < GT * GT; e += 256) {
-        const int r = e / GT, c = e - r * GT;
+    int x0, y0, np;
+    gauss_tile_coords(H, W, x0, y0, np);
+    const T* m = avg + (size_t)np * H * W;
+    gauss_tile(m, H, W, x0, y0, t);
+    for (int e = threadIdx.x; e < TW * TH; e += 256) {
+        const int r = e / TW, c = e - r * TW;
         const int y = y0 + r, x = x0 + c;
         if (y >= H || x >= W) continue;
         const double v = t.g[r + 1][c + 1];
@@ -137,152 +131,7 @@ __global__ __launch_bounds__(256) void gauss_nms(const T* __restrict__ avg, int 
             const int slot = atomicAdd(cnt + np, 1);
             if (slot < cap) {
                 list[(size_t)np * cap + slot] = y * W + x;
-                list_score[(size_t)np * cap + slot] = t.in[r + 13][c + 13];
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// Fused body heat chain: the scale-averaged full-resolution heat value
-//   heat_avg[y, x] = sum_s (double)(resize_s(x8 map_s)[y, x] / n_scales)     (src/body.py:55-67)
-// is evaluated on the fly from the x8 maps while the Gaussian tile is loaded, so the 18 float64
-// full-resolution maps are never written or re-read.  The 25-tap passes use per-thread
-// register windows (one LDS read per output instead of 25); the arithmetic order is scipy's.
-__device__ __forceinline__ double heat_avg_at(const PafScales& S, int n, int ch, int Y, int X) {
-    double acc = 0.0;
-    for (int s = 0; s < S.n; ++s) {
-        const float* plane = S.mid[s] + ((size_t)n * S.cm + ch) * S.hs[s] * S.ws[s];
-        float v;
-        if (S.hs[s] == S.H && S.ws[s] == S.W) {
-            v = plane[(size_t)Y * S.ws[s] + X];
-        } else {
-            const CubicTap ty = cubic_tap(Y, S.sy[s], S.hs[s]);
-            const CubicTap tx = cubic_tap(X, S.sx[s], S.ws[s]);
-            v = cubic_sample_f32(plane, S.ws[s], ty, tx);
-        }
-        v = v / (float)S.n;
-        acc = acc + (double)v;
-    }
-    return acc;
-}
-
-__global__ __launch_bounds__(256) void gauss_nms_fused(PafScales S, int ch0, double thre, int cap,
-                                                       int* __restrict__ cnt, int* __restrict__ list,
-                                                       double* __restrict__ list_score) {
-    __shared__ GaussTile t;
-    __shared__ CubicTap s_ty[GI], s_tx[GI];  // per-tile resize taps of the (reflected) rows / cols
-    __shared__ int s_rlo, s_rhi;
-    constexpr int HB_ROWS = (GR * GI) / GI;   // horizontal-pass rows that fit in t.v (34)
-    float* hbuf = reinterpret_cast<float*>(&t.v[0][0]);  // [src row][tile col], reuses t.v
-    constexpr int HB_CAP = (int)(sizeof(t.v) / sizeof(float)) / GI;
-    (void)HB_ROWS;
-    const int tid = threadIdx.x;
-    const int x0 = blockIdx.x * GT, y0 = blockIdx.y * GT;
-    const int np = blockIdx.z;
-    const int n = np / 18, part = np - n * 18;
-    const int H = S.H, W = S.W;
-    for (int s = 0; s < S.n; ++s) {
-        const bool ident = S.hs[s] == S.H && S.ws[s] == S.W;
-        const float* plane = S.mid[s] + ((size_t)n * S.cm + ch0 + part) * S.hs[s] * S.ws[s];
-        if (ident) {
-            constexpr int IIT = (GI * GI + 255) / 256;
-            float iv[IIT];
-#pragma unroll
-            for (int it = 0; it < IIT; ++it) {
-                const int e = min(tid + it * 256, GI * GI - 1);
-                const int r = e / GI, c = e - r * GI;
-                iv[it] = plane[(size_t)reflect_idx(y0 - 13 + r, H) * S.ws[s] + reflect_idx(x0 - 13 + c, W)];
-            }
-#pragma unroll
-            for (int it = 0; it < IIT; ++it) {
-                const int e = tid + it * 256;
-                if (e < GI * GI) {
-                    const int r = e / GI, c = e - r * GI;
-                    const float v = iv[it] / (float)S.n;
-                    t.in[r][c] = (s == 0 ? 0.0 : t.in[r][c]) + (double)v;
-                }
-            }
-            __syncthreads();
-            continue;
-        }
-        if (tid < GI) s_ty[tid] = cubic_tap(reflect_idx(y0 - 13 + tid, H), S.sy[s], S.hs[s]);
-        else if (tid < 2 * GI) s_tx[tid - GI] = cubic_tap(reflect_idx(x0 - 13 + tid - GI, W), S.sx[s], S.ws[s]);
-        if (tid == 0) {
-            s_rlo = 0x7fffffff;
-            s_rhi = -1;
-        }
-        __syncthreads();
-        if (tid < GI) {
-            atomicMin(&s_rlo, s_ty[tid].i[0]);
-            atomicMax(&s_rhi, s_ty[tid].i[3]);
-        }
-        __syncthreads();
-        const int rlo = s_rlo, nrows = s_rhi - s_rlo + 1;
-        if (nrows <= HB_CAP) {
-            // OpenCV's separable order: horizontal interpolation of each needed source row once,
-            // then the vertical combination per output (identical float32 values).
-            // fixed trip count, fully unrolled: all 32 loads of a thread are in flight together
-            constexpr int HIT = (HB_CAP * GI + 255) / 256;
-            float hv[HIT][4];
-#pragma unroll
-            for (int it = 0; it < HIT; ++it) {
-                const int e = tid + it * 256;
-                const int rr = e / GI, c = e - rr * GI;
-                const bool ok = e < nrows * GI;
-                const float* row = plane + (size_t)(rlo + (ok ? rr : 0)) * S.ws[s];
-                const CubicTap& tx = s_tx[ok ? c : 0];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) hv[it][j] = row[tx.i[j]];
-            }
-#pragma unroll
-            for (int it = 0; it < HIT; ++it) {
-                const int e = tid + it * 256;
-                if (e < nrows * GI) {
-                    const CubicTap& tx = s_tx[e % GI];
-                    float v = hv[it][0] * tx.c[0];
-                    v = v + hv[it][1] * tx.c[1];
-                    v = v + hv[it][2] * tx.c[2];
-                    v = v + hv[it][3] * tx.c[3];
-                    hbuf[e] = v;
-                }
-            }
-            __syncthreads();
-            for (int e = tid; e < GI * GI; e += 256) {
-                const int r = e / GI, c = e - r * GI;
-                const CubicTap& ty = s_ty[r];
-                float v = hbuf[(ty.i[0] - rlo) * GI + c] * ty.c[0];
-                v = v + hbuf[(ty.i[1] - rlo) * GI + c] * ty.c[1];
-                v = v + hbuf[(ty.i[2] - rlo) * GI + c] * ty.c[2];
-                v = v + hbuf[(ty.i[3] - rlo) * GI + c] * ty.c[3];
-                v = v / (float)S.n;
-                t.in[r][c] = (s == 0 ? 0.0 : t.in[r][c]) + (double)v;
-            }
-        } else {  // strong downscale: direct 16-tap evaluation
-            for (int e = tid; e < GI * GI; e += 256) {
-                const int r = e / GI, c = e - r * GI;
-                float v = cubic_sample_f32(plane, S.ws[s], s_ty[r], s_tx[c]);
-                v = v / (float)S.n;
-                t.in[r][c] = (s == 0 ? 0.0 : t.in[r][c]) + (double)v;
-            }
-        }
-        __syncthreads();
-    }
-    gauss_passes(t);
-    for (int e = tid; e < GT * GT; e += 256) {
-        const int r = e / GT, c = e - r * GT;
-        const int y = y0 + r, x = x0 + c;
-        if (y >= H || x >= W) continue;
-        const double v = t.g[r + 1][c + 1];
-        const double up = y > 0 ? t.g[r][c + 1] : 0.0;
-        const double dn = y < H - 1 ? t.g[r + 2][c + 1] : 0.0;
-        const double lf = x > 0 ? t.g[r + 1][c] : 0.0;
-        const double rt = x < W - 1 ? t.g[r + 1][c + 2] : 0.0;
-        if (v >= up && v >= dn && v >= lf && v >= rt && v > thre) {
-            const int slot = atomicAdd(cnt + np, 1);
-            if (slot < cap) {
-                list[(size_t)np * cap + slot] = y * W + x;
-                list_score[(size_t)np * cap + slot] = t.in[r + 13][c + 13];  // map_ori[y, x]
+                list_score[(size_t)np * cap + slot] = (double)m[(size_t)y * W + x];  // map_ori[y, x]
             }
         }
     }
@@ -294,13 +143,13 @@ __global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict_
                                                        int* __restrict__ lab, int* __restrict__ cnt) {
     __shared__ GaussTile t;
     __shared__ int s_n;
-    const int x0 = blockIdx.x * GT, y0 = blockIdx.y * GT;
-    const int np = blockIdx.z;
+    int x0, y0, np;
+    gauss_tile_coords(H, W, x0, y0, np);
     if (threadIdx.x == 0) s_n = 0;
     gauss_tile(avg + (size_t)np * H * W, H, W, x0, y0, t);
     int mine = 0;
-    for (int e = threadIdx.x; e < GT * GT; e += 256) {
-        const int r = e / GT, c = e - r * GT;
+    for (int e = threadIdx.x; e < TW * TH; e += 256) {
+        const int r = e / TW, c = e - r * TW;
         const int y = y0 + r, x = x0 + c;
         if (y >= H || x >= W) continue;
         const bool on = t.g[r + 1][c + 1] > thre;
@@ -606,7 +455,7 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
 // ------------------------------------------------------------------ launchers
 void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
                       double* list_score, hipStream_t st) {
-    dim3 grid(((W + GT - 1) / GT) * ((H + GT - 1) / GT) * NP);
+    dim3 grid(((W + TW - 1) / TW) * ((H + TH - 1) / TH) * NP);
     if (f32)
         hipLaunchKernelGGL(gauss_nms<float>, grid, dim3(256), 0, st, (const float*)avg, 18, H, W, thre, cap, cnt, list,
                            list_score);
@@ -616,7 +465,7 @@ void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double th
 }
 
 void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st) {
-    dim3 grid((W + GT - 1) / GT, (H + GT - 1) / GT, NP);
+    dim3 grid(((W + TW - 1) / TW) * ((H + TH - 1) / TH) * NP);
     hipLaunchKernelGGL(gauss_threshold, grid, dim3(256), 0, st, avg, H, W, thre, lab, cnt);
 }
 
@@ -626,11 +475,6 @@ void launch_peaks_finalize(const int* cnt, const int* list, const double* list_s
                        part_cnt);
 }
 
-void launch_gauss_nms_fused(const PafScales& S, int N, int ch0, double thre, int cap, int* cnt, int* list,
-                            double* list_score, hipStream_t st) {
-    dim3 grid((S.W + GT - 1) / GT, (S.H + GT - 1) / GT, N * 18);
-    hipLaunchKernelGGL(gauss_nms_fused, grid, dim3(256), 0, st, S, ch0, thre, cap, cnt, list, list_score);
-}
 
 void launch_paf_score(const PafScales& S, const int* peak_pos, const int* part_cnt, int N, int cap, double thre2,
                       double* score, hipStream_t st) {

@@ -81,6 +81,15 @@ def test_conv_7x7_tiles(native, handle, cout, mt, pt, splits):
     _conv_case(native, handle, 3, 128, 23, 41, cout, 7, relu=True, mt=mt, pt=pt, splits=splits, seed=4)
 
 
+def test_conv_streamk_inkernel_reduction(native, monkeypatch):
+    # the opt-in in-kernel stream-K reduction (last arriving workgroup sums the parts)
+    monkeypatch.setenv("OPOSE_SK_INKERNEL", "1")
+    h = native.Handle(0)
+    for mt, pt, splits in ((128, 256, 7), (128, 128, 9), (64, 64, 13)):
+        _conv_case(native, h, 3, 128, 23, 41, 128, 7, relu=True, mt=mt, pt=pt, splits=splits, seed=6)
+    _conv_case(native, h, 2, 96, 17, 29, 256, 3, relu=False, mt=256, pt=128, splits=6, seed=5)
+
+
 @pytest.mark.parametrize("splits", [0, 1, 6])
 def test_conv_256_rows(native, handle, splits):
     _conv_case(native, handle, 2, 96, 17, 29, 256, 3, relu=False, mt=256, pt=128, splits=splits, seed=5)
