@@ -10,8 +10,9 @@
 // atomicMin linking larger roots under smaller ones).  skimage / scipy number components in
 // raster order of their first pixel, which is exactly the order of those minima, so
 // "first component with the maximal sum" is "smallest root with the maximal sum".
-// Component sums are float64 atomics (order differs from numpy's pairwise sum: only an exact
-// tie within ~1e-16 relative between two components could resolve differently).
+// Component sums: per wave one float64 atomic per distinct root (order differs from numpy's
+// pairwise sum: only an exact tie within ~1e-16 relative between two components could
+// resolve differently).
 #include "common.h"
 #include "kernels.h"
 
@@ -67,14 +68,29 @@ __global__ __launch_bounds__(256) void cc_compress_sum(int* __restrict__ lab, co
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     const int np = blockIdx.z;
-    if (x >= W) return;
     const size_t off = (size_t)np * H * W;
     int* L = lab + off;
     const int i = y * W + x;
-    if (L[i] < 0) return;
-    const int r = uf_find(L, i);
-    L[i] = r;
-    atomicAdd(sums + off + r, ori[off + i]);
+    int r = -1;
+    double v = 0.0;
+    if (x < W && L[i] >= 0) {
+        r = uf_find(L, i);
+        L[i] = r;
+        v = ori[off + i];
+    }
+    // one atomic per distinct root per wave (a component covers long runs of pixels: per-pixel
+    // float64 atomics on one address serialised the whole map)
+    bool active = r >= 0;
+    while (__any(active)) {
+        const unsigned long long m = __ballot(active);
+        const int src = __ffsll((long long)m) - 1;
+        const int rr = __shfl(r, src);
+        const bool mine = active && r == rr;
+        double sv = mine ? v : 0.0;
+        for (int o = 32; o >= 1; o >>= 1) sv += __shfl_xor(sv, o);
+        if ((int)(threadIdx.x & 63) == src) atomicAdd(sums + off + rr, sv);
+        active = active && !mine;
+    }
 }
 
 // one workgroup per (crop, part): pick the component, then the first row-major maximum of

@@ -1,0 +1,97 @@
+"""Secondary measurements for BASELINE.json configs C2, C3 and C5 on one MI355X (bench.py is
+the driver's C2/C4 throughput line).  Prints one JSON object; synthetic frames and seeded
+weights (BENCH_OUT_SCALE calibration for the body net) as in bench.py.
+
+C2  Body() on one 368x656 frame: host-in/host-out latency (PCIe included) and the
+    device-resident batch-1 path (infer_records).
+C3  Body()+Hand() per frame (src.pipeline.motion_data_every_frame, mode "bodyhand": hands of
+    the selected person, 368x368-class crops, 4 hand scales) and Hand() alone on a 368x368 crop.
+C5  1920x1080 frames with scale_search [0.5, 1.0, 1.5, 2.0] (averaged heat maps), device
+    resident batches -> frames/s per GPU (C5 shards frames over 8 GPUs like C4).
+"""
+from __future__ import annotations
+
+import copy
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "pytorch-openpose_amd"))
+from src.body import Body  # noqa: E402
+from src.hand import Hand  # noqa: E402
+from src.pipeline import motion_data_every_frame  # noqa: E402
+from src.weights import BENCH_OUT_SCALE, seeded_state_dict  # noqa: E402
+
+
+def timed(fn, iters, warm=2):
+    for _ in range(warm):
+        fn()
+    t = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        fn()
+        t.append(time.perf_counter() - t0)
+    return float(np.median(t)) * 1e3
+
+
+def main():
+    rng = np.random.default_rng(3)
+    out = {}
+    body = Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE))
+    hand = Hand(seeded_state_dict("hand", 0))
+    img = rng.integers(0, 256, (368, 656, 3), dtype=np.uint8)
+
+    # C2
+    out["C2_body_latency_ms"] = timed(lambda: body(img), 20)
+    dev = torch.device("cuda", 0)
+    f1 = torch.from_numpy(img[None].copy()).to(dev)
+    rec = torch.empty((1, body.handle.record_bytes()), dtype=torch.uint8, device=dev)
+
+    def dev1():
+        body.infer_records(f1, rec)
+        body.handle.synchronize()
+    out["C2_body_device_batch1_ms"] = timed(dev1, 20)
+
+    # C3
+    crop = rng.integers(0, 256, (368, 368, 3), dtype=np.uint8)
+    out["C3_hand_latency_ms"] = timed(lambda: hand(crop), 10)
+    n_hands = []
+
+    def pipe():
+        pose = motion_data_every_frame(body, hand, img, "bodyhand")
+        n_hands.append(int((pose[18:39, 2] > 0).any()) + int((pose[39:60, 2] > 0).any()))
+    out["C3_bodyhand_frame_ms"] = timed(pipe, 10)
+    out["C3_note"] = "hands found per frame (median over runs): %d" % int(np.median(n_hands))
+
+    # C5
+    # The 368x656 calibration carpets some heat channels at 1080p / 4 scales (plateaus above
+    # thre1); a -3.5 shift of the heat biases gives ~1-10 peaks per part (scripts/calib_c5.py).
+    # The network (value independent) is >97 % of this config's time.
+    cal = copy.deepcopy(BENCH_OUT_SCALE)
+    w, b = cal["Mconv7_stage6_L2"]
+    cal["Mconv7_stage6_L2"] = (w, [v - 3.5 for v in b])
+    body5 = Body(seeded_state_dict("body", 0, out_scale=cal), scale_search=(0.5, 1.0, 1.5, 2.0))
+    B = 4
+    f5 = torch.from_numpy(rng.integers(0, 256, (B, 1080, 1920, 3), dtype=np.uint8)).to(dev)
+    rec5 = torch.empty((B, body5.handle.record_bytes()), dtype=torch.uint8, device=dev)
+
+    def step5():
+        body5.infer_records(f5, rec5)
+        body5.handle.synchronize()
+    ms = timed(step5, 5, warm=1)
+    out["C5_1080p_4scale_batch"] = B
+    out["C5_1080p_4scale_ms_per_batch"] = ms
+    out["C5_1080p_4scale_frames_per_s_per_gpu"] = B / (ms * 1e-3)
+    st = rec5.view(torch.int32)[:, 0].cpu().numpy()
+    out["C5_status_nonzero"] = int((st != 0).sum())
+    out["C5_mean_peaks_people"] = rec5.view(torch.int32)[:, 1:3].float().mean(0).cpu().tolist()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
