@@ -156,7 +156,7 @@ struct opose_ctx {
     bool loaded[2] = {false, false};
     // workspace
     DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[kMaxScales], avg, cnt, list, peak_pos, part_cnt,
-        score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score, skcnt;
+        score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score, skcnt, hsel;
     // stream-K: split tiles reduced by the conv_sk_fixup launch (default) or in-kernel by the
     // last arriving workgroup (OPOSE_SK_INKERNEL=1; measured 0.4 % slower at batch 32: the
     // reducing workgroup's serial slab reads stall its next tile more than the launch costs)
@@ -903,7 +903,8 @@ static void hand_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     launch_gauss_threshold(avg, NP, H, W, p.thre_hand, lab, cnt, h->stream);
     h->prof_end(pe);
     h->prof_begin(pe, "hand_cc", 0, 0);
-    launch_hand_cc(avg, NP, H, W, lab, sums, cnt, pk, fd, h->stream);
+    void* ws = h->hsel.ensure<uint8_t>(hand_cc_workspace_bytes(NP), h->stream);
+    launch_hand_cc(avg, NP, H, W, lab, sums, cnt, pk, fd, ws, h->stream);
     h->prof_end(pe);
     if (!(flags & OPOSE_OUT_DEVICE)) {
         OPOSE_HIP_CHECK(hipMemcpyAsync(peaks_out, pk, sizeof(double) * NP * 3, hipMemcpyDeviceToHost, h->stream));

@@ -2,8 +2,8 @@
 //
 // Reference: hitmaxiang/pytorch-openpose src/hand.py:59-75 (per part):
 //   binary = gaussian_filter(map_ori, 3) > thre          (gauss_threshold in post.hip)
-//   label(binary, connectivity=2)                         => cc_union / cc_compress
-//   best = argmax_i sum(map_ori[label == i]) + 1          => cc_sums / hand_select
+//   label(binary, connectivity=2)                         => cc_union / cc_compress_sum
+//   best = argmax_i sum(map_ori[label == i]) + 1          => cc_compress_sum / hand_select_*
 //   map_ori[label != best] = 0; (y, x) = util.npmax(map_ori) (first row-major max)
 //
 // Labels: every component is represented by its minimum linear pixel index (union-find with
@@ -44,7 +44,12 @@ __device__ __forceinline__ void uf_union(int* L, int a, int b) {
     }
 }
 
-// lab: [NP][H*W] seeds (index or -1); 8-connectivity: link to left, up-left, up, up-right
+// lab: [NP][H*W] seeds (-1, or the start of the pixel's run within its 64-pixel row segment,
+// see gauss_threshold).  8-connectivity with one union per run contact instead of four per
+// pixel: a run is already one tree, so a pixel whose left neighbour is set only links an
+// up-right pixel that starts a new run above (its left neighbour covers up-left and up);
+// a run start links the first pixel of each run above it; runs crossing a 64-pixel segment
+// boundary are joined at the boundary.
 __global__ __launch_bounds__(256) void cc_union(int* __restrict__ lab, int H, int W) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
@@ -53,12 +58,16 @@ __global__ __launch_bounds__(256) void cc_union(int* __restrict__ lab, int H, in
     int* L = lab + (size_t)np * H * W;
     const int i = y * W + x;
     if (L[i] < 0) return;
-    if (x > 0 && L[i - 1] >= 0) uf_union(L, i, i - 1);
+    const bool left = x > 0 && L[i - 1] >= 0;
+    if (left && (x & 63) == 0) uf_union(L, i, i - 1);  // run continues across the segment edge
     if (y > 0) {
         const int u = i - W;
-        if (x > 0 && L[u - 1] >= 0) uf_union(L, i, u - 1);
-        if (L[u] >= 0) uf_union(L, i, u);
-        if (x + 1 < W && L[u + 1] >= 0) uf_union(L, i, u + 1);
+        const bool ul = x > 0 && L[u - 1] >= 0, up = L[u] >= 0, ur = x + 1 < W && L[u + 1] >= 0;
+        if (!left) {
+            if (ul) uf_union(L, i, u - 1);
+            if (up && !ul) uf_union(L, i, u);
+        }
+        if (ur && !up) uf_union(L, i, u + 1);
     }
 }
 
@@ -93,19 +102,72 @@ __global__ __launch_bounds__(256) void cc_compress_sum(int* __restrict__ lab, co
     }
 }
 
-// one workgroup per (crop, part): pick the component, then the first row-major maximum of
-// {map_ori inside it, 0 elsewhere}; writes peaks[np] = (x, y, value), found[np]
-__global__ __launch_bounds__(256) void hand_select(const int* __restrict__ lab, const double* __restrict__ ori,
-                                                   const double* __restrict__ sums, const int* __restrict__ cnt,
-                                                   int H, int W, double* __restrict__ peaks, int* __restrict__ found) {
-    const int np = blockIdx.x;
+// Selection (src/hand.py:66-75), spread over SEL_NB workgroups per (crop, part):
+// pass 1: the component with the largest sum (ties: smallest root = lowest label);
+// pass 2: the first row-major maximum of {map_ori inside it, 0 elsewhere} (util.npmax).
+// Each pass: per-slice (value, index) partials, then a one-wave reduction.  The (greater
+// value, else smaller index) rule is associative, so the result is order independent.
+constexpr int SEL_NB = 32;
+
+__device__ __forceinline__ void better(double& v, int& i, double ov, int oi) {
+    if (ov > v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+    }
+}
+
+template <int PASS>
+__global__ __launch_bounds__(256) void hand_select_part(const int* __restrict__ lab, const double* __restrict__ ori,
+                                                        const double* __restrict__ sums, const int* __restrict__ cnt,
+                                                        const int* __restrict__ best, int n,
+                                                        double* __restrict__ part_v, int* __restrict__ part_i) {
+    const int b = blockIdx.x, np = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const size_t off = (size_t)np * H * W;
-    const int n = H * W;
+    if (cnt[np] == 0) return;
+    const size_t off = (size_t)np * n;
+    const int chunk = (n + SEL_NB - 1) / SEL_NB;
+    const int i0 = b * chunk, i1 = min(n, i0 + chunk);
+    const int bc = PASS == 2 ? best[np] : 0;
+    double v = -INFINITY;
+    int idx = 0x7fffffff;
+    for (int i = i0 + tid; i < i1; i += 256) {  // ascending per thread: ties keep the smaller
+        const int l = lab[off + i];
+        if (PASS == 1) {
+            if (l == i && sums[off + i] > v) {
+                v = sums[off + i];
+                idx = i;
+            }
+        } else {
+            const double x = l == bc ? ori[off + i] : 0.0;
+            if (x > v) {
+                v = x;
+                idx = i;
+            }
+        }
+    }
+    for (int o = 32; o >= 1; o >>= 1) better(v, idx, __shfl_xor(v, o), __shfl_xor(idx, o));
     __shared__ double s_v[4];
     __shared__ int s_i[4];
+    if (lane == 0) {
+        s_v[wave] = v;
+        s_i[wave] = idx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < 4; ++w) better(v, idx, s_v[w], s_i[w]);
+        part_v[np * SEL_NB + b] = v;
+        part_i[np * SEL_NB + b] = idx;
+    }
+}
+
+// one wave per (crop, part): reduce the SEL_NB partials
+template <int PASS>
+__global__ __launch_bounds__(64) void hand_select_reduce(const int* __restrict__ cnt, const double* __restrict__ part_v,
+                                                         const int* __restrict__ part_i, int W, int* __restrict__ best,
+                                                         double* __restrict__ peaks, int* __restrict__ found) {
+    const int np = blockIdx.x, lane = threadIdx.x;
     if (cnt[np] == 0) {  // nothing above threshold: the reference's [0, 0, 0] row
-        if (tid == 0) {
+        if (PASS == 2 && lane == 0) {
             peaks[np * 3 + 0] = 0.0;
             peaks[np * 3 + 1] = 0.0;
             peaks[np * 3 + 2] = 0.0;
@@ -113,69 +175,38 @@ __global__ __launch_bounds__(256) void hand_select(const int* __restrict__ lab, 
         }
         return;
     }
-    auto reduce = [&](double& v, int& idx) {
-        for (int o = 32; o >= 1; o >>= 1) {
-            const double ov = __shfl_xor(v, o);
-            const int oi = __shfl_xor(idx, o);
-            if (ov > v || (ov == v && oi < idx)) {
-                v = ov;
-                idx = oi;
-            }
-        }
-        if (lane == 0) {
-            s_v[wave] = v;
-            s_i[wave] = idx;
-        }
-        __syncthreads();
-        v = s_v[0];
-        idx = s_i[0];
-        for (int w = 1; w < 4; ++w)
-            if (s_v[w] > v || (s_v[w] == v && s_i[w] < idx)) {
-                v = s_v[w];
-                idx = s_i[w];
-            }
-        __syncthreads();
-    };
-    // 1) component with the largest sum (ties: smallest root = lowest label)
-    double bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int i = tid; i < n; i += 256) {
-        if (lab[off + i] == i) {
-            const double v = sums[off + i];
-            if (v > bv) {  // ascending i per thread: ties keep the smaller root
-                bv = v;
-                bi = i;
-            }
-        }
-    }
-    reduce(bv, bi);
-    const int best = bi;
-    // 2) first maximum of the masked map (everything outside the component reads 0.0)
-    double mv = -INFINITY;
-    int mi = 0x7fffffff;
-    for (int i = tid; i < n; i += 256) {
-        const double v = lab[off + i] == best ? ori[off + i] : 0.0;
-        if (v > mv) {
-            mv = v;
-            mi = i;
-        }
-    }
-    reduce(mv, mi);
-    if (tid == 0) {
-        peaks[np * 3 + 0] = (double)(mi % W);
-        peaks[np * 3 + 1] = (double)(mi / W);
-        peaks[np * 3 + 2] = mv;
+    double v = lane < SEL_NB ? part_v[np * SEL_NB + lane] : -INFINITY;
+    int idx = lane < SEL_NB ? part_i[np * SEL_NB + lane] : 0x7fffffff;
+    for (int o = 32; o >= 1; o >>= 1) better(v, idx, __shfl_xor(v, o), __shfl_xor(idx, o));
+    if (lane != 0) return;
+    if (PASS == 1) {
+        best[np] = idx;
+    } else {
+        peaks[np * 3 + 0] = (double)(idx % W);
+        peaks[np * 3 + 1] = (double)(idx / W);
+        peaks[np * 3 + 2] = v;
         found[np] = 1;
     }
 }
 
+size_t hand_cc_workspace_bytes(int NP) { return (size_t)NP * SEL_NB * (sizeof(double) + sizeof(int)) + NP * 4; }
+
 void launch_hand_cc(double* avg, int NP, int H, int W, int* lab, double* sums, const int* cnt, double* peaks,
-                    int* found, hipStream_t st) {
+                    int* found, void* ws, hipStream_t st) {
     dim3 grid((W + 255) / 256, H, NP);
     hipLaunchKernelGGL(cc_union, grid, dim3(256), 0, st, lab, H, W);
     OPOSE_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(double) * (size_t)NP * H * W, st));
     hipLaunchKernelGGL(cc_compress_sum, grid, dim3(256), 0, st, lab, avg, H, W, sums);
-    hipLaunchKernelGGL(hand_select, dim3(NP), dim3(256), 0, st, lab, avg, sums, cnt, H, W, peaks, found);
+    double* part_v = static_cast<double*>(ws);
+    int* part_i = reinterpret_cast<int*>(part_v + (size_t)NP * SEL_NB);
+    int* best = part_i + (size_t)NP * SEL_NB;
+    const int n = H * W;
+    hipLaunchKernelGGL(hand_select_part<1>, dim3(SEL_NB, NP), dim3(256), 0, st, lab, avg, sums, cnt, best, n, part_v,
+                       part_i);
+    hipLaunchKernelGGL(hand_select_reduce<1>, dim3(NP), dim3(64), 0, st, cnt, part_v, part_i, W, best, peaks, found);
+    hipLaunchKernelGGL(hand_select_part<2>, dim3(SEL_NB, NP), dim3(256), 0, st, lab, avg, sums, cnt, best, n, part_v,
+                       part_i);
+    hipLaunchKernelGGL(hand_select_reduce<2>, dim3(NP), dim3(64), 0, st, cnt, part_v, part_i, W, best, peaks, found);
 }
 
 }  // namespace opose

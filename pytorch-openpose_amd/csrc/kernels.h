@@ -49,7 +49,8 @@ void launch_assemble(const Conn* conn, const int* conn_cnt, const int* part_cnt,
                      uint8_t* records, hipStream_t st);
 
 // hand.hip
+size_t hand_cc_workspace_bytes(int NP);
 void launch_hand_cc(double* avg, int NP, int H, int W, int* lab, double* sums, const int* cnt, double* peaks,
-                    int* found, hipStream_t st);
+                    int* found, void* ws, hipStream_t st);
 
 }  // namespace opose

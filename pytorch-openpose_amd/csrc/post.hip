@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void gauss_nms(const T* __restrict__ avg, int 
 }
 
 // Hand: binary = gaussian_filter(map) > thre (src/hand.py:62-63) as union-find seeds:
-// lab[i] = i where set, -1 elsewhere; cnt[np] += #set.
+// lab[i] = start of i's run within its 64-pixel segment where set, -1 elsewhere; cnt[np] += #set.
 __global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict__ avg, int H, int W, double thre,
                                                        int* __restrict__ lab, int* __restrict__ cnt) {
     __shared__ GaussTile t;
@@ -148,13 +148,19 @@ __global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict_
     if (threadIdx.x == 0) s_n = 0;
     gauss_tile(avg + (size_t)np * H * W, H, W, x0, y0, t);
     int mine = 0;
+    // a wave = one 64-pixel row segment of the tile: each set pixel points at the start of its
+    // run inside the segment (union-find parent < itself), so cc_union only links runs
+    const int lane = threadIdx.x & 63;
     for (int e = threadIdx.x; e < TW * TH; e += 256) {
         const int r = e / TW, c = e - r * TW;
         const int y = y0 + r, x = x0 + c;
-        if (y >= H || x >= W) continue;
-        const bool on = t.g[r + 1][c + 1] > thre;
+        const bool in = y < H && x < W;
+        const bool on = in && t.g[r + 1][c + 1] > thre;
+        const unsigned long long unset = ~__ballot(on) & ((1ull << lane) - 1);  // unset lanes below
+        const int start = unset ? 64 - __clzll((long long)unset) : 0;          // first lane of the run
+        if (!in) continue;
         const int i = y * W + x;
-        lab[(size_t)np * H * W + i] = on ? i : -1;
+        lab[(size_t)np * H * W + i] = on ? i - (lane - start) : -1;
         mine += on;
     }
     if (mine) atomicAdd(&s_n, mine);

@@ -61,3 +61,28 @@ def test_hand_batch_and_all_missing(hand):
     from src.hand import _as_reference_array
     z = _as_reference_array(np.zeros((21, 3)), np.zeros(21, np.int32))
     assert z.dtype == np.int64 and not z.any()
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_hand_post_intricate_components(hand, seed):
+    """Heat maps hovering around the threshold: many components with holes, diagonal-only
+    contacts and long snakes after the x8 upsample + Gaussian -- the labelling, the sums and
+    the selection must match the oracle (scipy.ndimage.label) exactly."""
+    from scipy.ndimage import gaussian_filter
+    from oracle import hand_post
+    from oracle.body_post import preprocess
+    rng = np.random.default_rng(100 + seed)
+    S = 120
+    maps, lowres, pads = [], [], []
+    for s in SCALES:
+        _, pad, padded_hw = preprocess(np.zeros((S, S, 3), np.uint8), s * 368 / S)
+        h, w = padded_hw[0] // 8, padded_hw[1] // 8
+        noise = gaussian_filter(rng.standard_normal((22, h, w)), (0, 0.7, 0.7))
+        heat = (0.03 + 0.08 * noise / noise.std()).astype(np.float32)
+        maps.append(heat[None])
+        lowres.append((heat, pad, padded_hw))
+        pads.append(pad)
+    ref = hand_post.post_from_lowres((S, S), lowres)
+    out = hand.post(maps, pads, S, S)[0]
+    assert out.dtype == ref.dtype
+    assert np.array_equal(out, ref)
