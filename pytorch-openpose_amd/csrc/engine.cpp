@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -92,6 +93,10 @@ std::vector<Spec> state_dict_order(int net) {
 int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
 // ---------------------------------------------------------------- device memory helpers
+// Bumped whenever device memory that a captured hipGraph may reference is (re)allocated:
+// graphs captured under an older epoch are dropped instead of replayed.
+std::atomic<uint64_t> g_alloc_epoch{1};
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -110,6 +115,7 @@ struct DevBuf {
             size_t nb = std::max(b, bytes + bytes / 4);
             OPOSE_HIP_CHECK(hipMalloc(&p, nb));
             bytes = nb;
+            g_alloc_epoch.fetch_add(1);
         }
         return static_cast<T*>(p);
     }
@@ -145,7 +151,17 @@ struct ProfAgg {
 
 }  // namespace
 
+struct GraphEntry {
+    hipGraphExec_t exec = nullptr;
+    uint64_t epoch = 0;
+};
+
 struct opose_ctx {
+    // launch-sequence cache: per call signature, the device work of the first call runs
+    // eagerly (allocating every buffer), the second is captured into a hipGraph, later calls
+    // replay it (one launch instead of ~150: single-frame latency is launch bound)
+    std::map<std::string, GraphEntry> graphs;
+    bool use_graphs = getenv("OPOSE_NO_GRAPH") == nullptr;
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
@@ -220,6 +236,8 @@ struct opose_ctx {
         pending.clear();
     }
     ~opose_ctx() {
+        for (auto& kv : graphs)
+            if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
         for (auto e : event_pool) (void)hipEventDestroy(e);
         if (own_stream) (void)hipStreamDestroy(own_stream);
     }
@@ -276,8 +294,15 @@ TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK) {
         if (grid >= 1 && grid != tiles) {
             const double per_wg = (double)iters / grid;
             const double cu_load = std::max(floor1, std::ceil(grid / 256.0)) * per_wg * unit;
-            const long split = std::min<long>(tiles, 2 * grid);                 // tiles with partials
-            const double slab_bytes = (double)split * mt * pt * 4.0 * 3.0;       // write + re-read + out
+            // partial slabs: every workgroup segment that is not a whole tile writes one, the
+            // fixup re-reads them all (grid > tiles: ~grid + tiles segments, each tile cut in
+            // grid / tiles parts -- the dominant cost of tiny single-frame layers)
+            // (measured: with grid <= 2 x tiles the slabs stay cache resident and the old
+            // tiles-with-partials estimate ranks configurations better)
+            const long segs = grid > 2 * tiles ? grid + tiles : std::min<long>(tiles, 2 * grid);
+            const double slab_bytes = grid > 2 * tiles
+                                          ? (double)segs * mt * pt * 4.0 * 2.0 + (double)tiles * mt * pt * 4.0
+                                          : (double)segs * mt * pt * 4.0 * 3.0;
             const double sk = cu_load + slab_bytes / 5e12 / 0.42e-6 + 8.0;      // + fixup launch
             if (sk < best_cost * 0.97) {
                 best_cost = sk;
@@ -340,6 +365,7 @@ static void upload_conv(opose_ctx* h, int net, const std::string& key, const std
     OPOSE_HIP_CHECK(hipMalloc(&dc->wt, wt.size() * 4));
     OPOSE_HIP_CHECK(hipMalloc(&dc->bias, bias.size() * 4));
     OPOSE_HIP_CHECK(hipMalloc(&dc->ktab, ktab.size() * 4));
+    g_alloc_epoch.fetch_add(1);  // captured graphs may hold the replaced layer's pointers
     OPOSE_HIP_CHECK(hipMemcpy(dc->wt, wt.data(), wt.size() * 4, hipMemcpyHostToDevice));
     OPOSE_HIP_CHECK(hipMemcpy(dc->bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
     OPOSE_HIP_CHECK(hipMemcpy(dc->ktab, ktab.data(), ktab.size() * 4, hipMemcpyHostToDevice));
@@ -638,6 +664,63 @@ static int worst_status(const uint8_t* rec, int N, size_t bytes) {
         return OPOSE_E_WEIGHTS;                \
     }
 
+// Run `work` (device work only: kernels, device memsets/copies on h->stream, no host sync,
+// no allocation once warm) through the launch-sequence cache keyed by `key`.
+template <class F>
+static void run_graphed(opose_ctx* h, const std::string& key, F&& work) {
+    if (!h->use_graphs || h->prof || !h->stream) {
+        work();
+        return;
+    }
+    const uint64_t epoch = g_alloc_epoch.load();
+    auto it = h->graphs.find(key);
+    if (it != h->graphs.end() && it->second.exec && it->second.epoch == epoch) {
+        OPOSE_HIP_CHECK(hipGraphLaunch(it->second.exec, h->stream));
+        return;
+    }
+    if (it == h->graphs.end() || it->second.epoch != epoch) {  // first sighting: eager, allocates
+        if (it != h->graphs.end() && it->second.exec) OPOSE_HIP_CHECK(hipGraphExecDestroy(it->second.exec));
+        work();
+        h->graphs[key] = GraphEntry{nullptr, g_alloc_epoch.load()};
+        return;
+    }
+    // second sighting with nothing reallocated since: capture, instantiate, launch
+    OPOSE_HIP_CHECK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    try {
+        work();
+    } catch (...) {
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(h->stream, &g);
+        if (g) (void)hipGraphDestroy(g);
+        throw;
+    }
+    hipGraph_t g = nullptr;
+    OPOSE_HIP_CHECK(hipStreamEndCapture(h->stream, &g));
+    if (g_alloc_epoch.load() != epoch) {  // something allocated inside the capture: not replayable
+        (void)hipGraphDestroy(g);
+        h->graphs.erase(key);
+        work();
+        return;
+    }
+    hipGraphExec_t ex = nullptr;
+    const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    OPOSE_HIP_CHECK(e);
+    it->second.exec = ex;
+    OPOSE_HIP_CHECK(hipGraphLaunch(ex, h->stream));
+}
+
+static std::string call_key(const char* what, int N, int H, int W, int64_t rs, int64_t fs, const opose_params& p,
+                            const void* in_dev, const void* out_dev, int ppp, int maxp) {
+    std::string k(what);
+    char tmp[256];
+    std::snprintf(tmp, sizeof tmp, "|%d|%d|%d|%lld|%lld|%p|%p|%d|%d|", N, H, W, (long long)rs, (long long)fs, in_dev,
+                  out_dev, ppp, maxp);
+    k += tmp;
+    k.append(reinterpret_cast<const char*>(&p), sizeof p);
+    return k;
+}
+
 extern "C" {
 
 void opose_default_params(int net, opose_params* p) {
@@ -828,20 +911,23 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
         }
         std::vector<ScaleGeom> gs;
         for (int s = 0; s < p.n_scales; ++s) gs.push_back(geom(p.scales[s], p, H, W));
-        for (int s = 0; s < p.n_scales; ++s) {
-            const ScaleGeom& g = gs[s];
-            float* x = h->x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
-            ProfEntry pe;
-            h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
-            launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp, g.Wp,
-                              (float)p.pad_value / 256.f - 0.5f, x, h->stream);
-            h->prof_end(pe);
-            float* S = body_net(h, x, N, g.Hp, g.Wp);
-            upsample_to_mid(h, s, S, 185, N, g, 56);
-        }
         uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)
                                                   : h->records.ensure<uint8_t>(L.bytes * N, h->stream);
-        body_post_common(h, N, H, W, gs, p, rec);
+        const std::string key = call_key("body", N, H, W, row_stride, frame_stride, p, fd, rec, h->ppp, h->maxp);
+        run_graphed(h, key, [&] {
+            for (int s = 0; s < p.n_scales; ++s) {
+                const ScaleGeom& g = gs[s];
+                float* x = h->x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
+                ProfEntry pe;
+                h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
+                launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp,
+                                  g.Wp, (float)p.pad_value / 256.f - 0.5f, x, h->stream);
+                h->prof_end(pe);
+                float* S = body_net(h, x, N, g.Hp, g.Wp);
+                upsample_to_mid(h, s, S, 185, N, g, 56);
+            }
+            body_post_common(h, N, H, W, gs, p, rec);
+        });
         return finish_records(h, N, records, rec, flags);
     });
 }
@@ -906,9 +992,16 @@ static void hand_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     void* ws = h->hsel.ensure<uint8_t>(hand_cc_workspace_bytes(NP), h->stream);
     launch_hand_cc(avg, NP, H, W, lab, sums, cnt, pk, fd, ws, h->stream);
     h->prof_end(pe);
+}
+
+// copy the hand results to the host (unless they were written to device buffers)
+static void hand_finish(opose_ctx* h, int N, double* peaks_out, int32_t* found_out, int flags) {
+    const int NP = N * 21;
     if (!(flags & OPOSE_OUT_DEVICE)) {
-        OPOSE_HIP_CHECK(hipMemcpyAsync(peaks_out, pk, sizeof(double) * NP * 3, hipMemcpyDeviceToHost, h->stream));
-        OPOSE_HIP_CHECK(hipMemcpyAsync(found_out, fd, sizeof(int) * NP, hipMemcpyDeviceToHost, h->stream));
+        OPOSE_HIP_CHECK(hipMemcpyAsync(peaks_out, h->hpeaks.ensure<double>((size_t)NP * 3, h->stream),
+                                       sizeof(double) * NP * 3, hipMemcpyDeviceToHost, h->stream));
+        OPOSE_HIP_CHECK(hipMemcpyAsync(found_out, h->hfound.ensure<int>((size_t)NP, h->stream), sizeof(int) * NP,
+                                       hipMemcpyDeviceToHost, h->stream));
         OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
     }
     h->prof_drain();
@@ -929,18 +1022,26 @@ int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
         }
         std::vector<ScaleGeom> gs;
         for (int s = 0; s < p.n_scales; ++s) gs.push_back(geom(p.scales[s], p, H, W));
-        for (int s = 0; s < p.n_scales; ++s) {
-            const ScaleGeom& g = gs[s];
-            float* x = h->x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
-            ProfEntry pe;
-            h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
-            launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp, g.Wp,
-                              (float)p.pad_value / 256.f - 0.5f, x, h->stream);
-            h->prof_end(pe);
-            float* Sb = hand_net(h, x, N, g.Hp, g.Wp);
-            upsample_to_mid(h, s, Sb, 150, N, g, 21);
-        }
-        hand_post_common(h, N, H, W, gs, p, peaks, found, flags & OPOSE_OUT_DEVICE);
+        const bool od = flags & OPOSE_OUT_DEVICE;
+        char fk[32];
+        std::snprintf(fk, sizeof fk, "%p", od ? (const void*)found : nullptr);
+        const std::string key =
+            call_key("hand", N, H, W, row_stride, frame_stride, p, fd, od ? (const void*)peaks : nullptr, 0, 0) + fk;
+        run_graphed(h, key, [&] {
+            for (int s = 0; s < p.n_scales; ++s) {
+                const ScaleGeom& g = gs[s];
+                float* x = h->x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
+                ProfEntry pe;
+                h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
+                launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp,
+                                  g.Wp, (float)p.pad_value / 256.f - 0.5f, x, h->stream);
+                h->prof_end(pe);
+                float* Sb = hand_net(h, x, N, g.Hp, g.Wp);
+                upsample_to_mid(h, s, Sb, 150, N, g, 21);
+            }
+            hand_post_common(h, N, H, W, gs, p, peaks, found, flags & OPOSE_OUT_DEVICE);
+        });
+        hand_finish(h, N, peaks, found, flags & OPOSE_OUT_DEVICE);
     });
     return OPOSE_OK;
 }
@@ -978,6 +1079,7 @@ int opose_hand_post(opose_t* h, const float* const* maps, const int* hl, const i
             gs.push_back(g);
         }
         hand_post_common(h, N, H, W, gs, p, peaks, found, flags & OPOSE_OUT_DEVICE);
+        hand_finish(h, N, peaks, found, flags & OPOSE_OUT_DEVICE);
     });
     return OPOSE_OK;
 }

@@ -261,3 +261,20 @@ def test_tiny_frames_vs_oracle(body, hw):
     if cand.size:
         assert np.array_equal(cand[:, [0, 1, 3]], ref_c[:, [0, 1, 3]])
     assert np.array_equal(subset[:, :18], ref_s[:, :18])
+
+
+def test_graph_replay_matches_eager(native):
+    """The launch-sequence cache: call 1 eager, call 2 captured, calls 3+ replayed -- all equal,
+    also when two shapes alternate and when a larger shape reallocates the workspace."""
+    from src.body import Body
+    from src.weights import BENCH_OUT_SCALE, seeded_state_dict
+    body = Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE))
+    rng = np.random.default_rng(9)
+    a = rng.integers(0, 256, (184, 328, 3), dtype=np.uint8)
+    b = rng.integers(0, 256, (120, 200, 3), dtype=np.uint8)
+    big = rng.integers(0, 256, (368, 656, 3), dtype=np.uint8)
+    ra, rb = body(a), body(b)
+    for img, ref in ((a, ra), (b, rb), (a, ra), (b, rb), (big, None), (a, ra), (a, ra), (b, rb)):
+        out = body(img)
+        if ref is not None:
+            assert np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1])
