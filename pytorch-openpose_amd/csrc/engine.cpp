@@ -162,6 +162,13 @@ struct opose_ctx {
     // replay it (one launch instead of ~150: single-frame latency is launch bound)
     std::map<std::string, GraphEntry> graphs;
     bool use_graphs = getenv("OPOSE_NO_GRAPH") == nullptr;
+    // conv_window_f32 for eligible 3x3 / 7x7 layers, opt-in (OPOSE_CONV_WINDOW=1): it cuts the
+    // activation DMA 25x but measured 1-3 % slower than the im2col kernel at batch 32 -- the
+    // kernel is MFMA/clock bound (85 % MFMA busy at ~1.8-2.0 GHz under load), not load bound
+    bool conv_window = [] {
+        const char* e = getenv("OPOSE_CONV_WINDOW");
+        return e && e[0] == '1';
+    }();
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
@@ -428,7 +435,7 @@ static void run_conv(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W
     if (h->detail)
         pe.detail = "layer/" + c0->name + "/" + std::to_string(t.mt) + "x" + std::to_string(t.pt) + "s" +
                     std::to_string(t.grid) + "/n" + std::to_string(a.npix);
-    launch_conv(a, c0->ktab, t.mt, t.pt, h->stream);
+    if (!(h->conv_window && launch_conv_window(a, t.mt, t.pt, h->stream))) launch_conv(a, c0->ktab, t.mt, t.pt, h->stream);
     h->prof_end(pe);
 }
 
@@ -1114,7 +1121,7 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
         a.sk_grid = t.grid;
         a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
         a.sk_cnt = h->sk_counters((a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * a.ngroups);
-        launch_conv(a, c->ktab, t.mt, t.pt, h->stream);
+        if (!(h->conv_window && launch_conv_window(a, t.mt, t.pt, h->stream))) launch_conv(a, c->ktab, t.mt, t.pt, h->stream);
         OPOSE_HIP_CHECK(hipMemcpyAsync(out, yd, ny * 4, hipMemcpyDeviceToHost, h->stream));
         OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
         h->convs[0].erase("__debug__");
@@ -1163,7 +1170,7 @@ int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, in
                     throw std::invalid_argument("ablations exist for the 128x128 7x7 kernel only");
                 launch_conv_ablation(a, ablate, h->stream);
             } else {
-                launch_conv(a, c->ktab, t.mt, t.pt, h->stream);
+                if (!(h->conv_window && launch_conv_window(a, t.mt, t.pt, h->stream))) launch_conv(a, c->ktab, t.mt, t.pt, h->stream);
             }
         };
         go();  // warm-up

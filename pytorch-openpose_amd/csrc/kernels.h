@@ -20,6 +20,9 @@ struct Conn {
 };
 
 // conv.hip
+// window variant (3x3 / 7x7, 128x256 tiles, short rows); false: not applicable, nothing launched
+size_t conv_window_lds_bytes(int mt, int pt, int ks, int W);
+bool launch_conv_window(const ConvArgs& a, int mt, int pt, hipStream_t st);
 void launch_conv(const ConvArgs& a, const int* ktab, int mt, int pt, hipStream_t st);
 void launch_conv_ablation(const ConvArgs& a, int ablate, hipStream_t st);
 void launch_fill_hash(float* p, size_t n, uint32_t seed, hipStream_t st);

@@ -278,3 +278,26 @@ def test_graph_replay_matches_eager(native):
         out = body(img)
         if ref is not None:
             assert np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1])
+
+
+@pytest.mark.parametrize("N,Cin,H,W,Cout,ks,splits", [
+    (1, 185, 23, 41, 256, 7, 0),    # Mconv1: padded channel block, two M tiles
+    (20, 64, 5, 6, 128, 7, 0),      # windows spanning many tiny frames (halo > frame)
+    (3, 128, 23, 41, 128, 7, 11),   # stream-K ranges starting mid channel block
+    (2, 256, 46, 82, 256, 3, 0),    # conv3_x rows (window 422 floats)
+    (1, 64, 9, 200, 100, 3, 3),     # wide rows, M = 100 padded to 128
+])
+def test_conv_window_kernel(native, window_handle, N, Cin, H, W, Cout, ks, splits):
+    # opt-in conv_window_f32 (flat activation window per channel block) on 128x256 tiles
+    _conv_case(native, window_handle, N, Cin, H, W, Cout, ks, relu=True, mt=128, pt=256, splits=splits, seed=7)
+    # and the default im2col kernel on the same case
+    _conv_case(native, native.Handle(0), N, Cin, H, W, Cout, ks, relu=True, mt=128, pt=256, splits=splits, seed=7)
+
+
+@pytest.fixture(scope="module")
+def window_handle(native):
+    os.environ["OPOSE_CONV_WINDOW"] = "1"
+    try:
+        return native.Handle(0)
+    finally:
+        del os.environ["OPOSE_CONV_WINDOW"]
