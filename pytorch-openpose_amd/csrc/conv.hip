@@ -664,7 +664,8 @@ __global__ void fill_hash(float* p, size_t n, uint32_t seed) {
         h ^= h >> 15;
         h *= 2246822519u;
         h ^= h >> 13;
-        p[i] = (float)(h & 0xffffff) / 8388608.f - 1.f;
+        const float v = (float)(h & 0xffffff) / 8388608.f - 1.f;
+        p[i] = (seed & 0x80000000u) ? fmaxf(v, 0.f) : v;  // top seed bit: ReLU-like (half zeros)
     }
 }
 

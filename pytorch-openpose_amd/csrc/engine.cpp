@@ -1144,7 +1144,9 @@ int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, in
         const size_t nx = (size_t)ngroups * N * Cin * H * W, ny = (size_t)ngroups * N * Cout * H * W;
         float* xd = xin.ensure<float>(nx, h->stream);
         float* yd = yout.ensure<float>(ny, h->stream);
-        launch_fill_hash(xd, nx, 3, h->stream);
+        // OPOSE_TIMING_RELU=1: activations with the ReLU sparsity of the real network (the chip
+        // holds a higher clock on half-zero operands than on dense noise)
+        launch_fill_hash(xd, nx, getenv("OPOSE_TIMING_RELU") ? 0x80000003u : 3u, h->stream);
         ConvArgs a{};
         a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.ks = ks; a.pad = ks / 2;
         a.K = c->K; a.Kpad = c->Kpad; a.Mpad = c->Mpad; a.npix = N * H * W;
