@@ -122,6 +122,16 @@ int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
                      int64_t frame_stride, const opose_params* p, double* peaks,
                      int32_t* found, int flags);
 
+/* Hand on n square crops of different sizes (the hands util.handDetect finds in a batch of
+ * frames): crops[i] = uint8 [sizes[i]][sizes[i]][3] with row stride row_strides[i].  Every
+ * crop maps to the same network input per scale (scale * boxsize), so the network runs once
+ * per scale for all crops; resize-back and component selection run per crop.  peaks [n][21][3],
+ * found [n][21]; same per-crop results as opose_hand_infer up to fp32 network noise.
+ * Replaces a loop of Hand.__call__ over crops (srcmx/MotionEstimation.py:186-201). */
+int opose_hand_infer_crops(opose_t* h, const uint8_t* const* crops, const int* sizes,
+                           const int64_t* row_strides, int n, const opose_params* p,
+                           double* peaks, int32_t* found, int flags);
+
 /* Post-network hand path: maps[s] = [N,22,hl[s],wl[s]] per scale s (pads per scale),
  * crop H x W. */
 int opose_hand_post(opose_t* h, const float* const* maps, const int* hl, const int* wl,

@@ -974,23 +974,30 @@ int opose_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int pa
 }
 
 // Hand post path from per-scale x8 maps (mids[s] = [N][21][Hs][Ws]) to peaks / found.
+// mid_crop: first crop of this call inside mids[s] (crop-batched hand path); out_crop: first
+// crop's slot in the peaks / found outputs
 static void hand_post_common(opose_ctx* h, int N, int H, int W, const std::vector<ScaleGeom>& gs,
-                             const opose_params& p, double* peaks_out, int32_t* found_out, int flags) {
+                             const opose_params& p, double* peaks_out, int32_t* found_out, int flags,
+                             int mid_crop = 0, int out_crop = 0) {
     const int ns = (int)gs.size();
     const int NP = N * 21;
     double* avg = h->avg.ensure<double>((size_t)NP * H * W, h->stream);
     ProfEntry pe;
     for (int s = 0; s < ns; ++s) {
         h->prof_begin(pe, "heat_full", 0, (double)NP * H * W * 8 * (s ? 2 : 1));
-        launch_heat_full(h->mids[s].ensure<float>(0, h->stream), 21, 0, 21, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy,
-                         gs[s].up_sx, ns, s > 0, avg, h->stream);
+        const float* mid = h->mids[s].ensure<float>(0, h->stream) + (size_t)mid_crop * 21 * gs[s].Hs * gs[s].Ws;
+        launch_heat_full(mid, 21, 0, 21, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx, ns, s > 0, avg,
+                         h->stream);
         h->prof_end(pe);
     }
     int* lab = h->hlab.ensure<int>((size_t)NP * H * W, h->stream);
     double* sums = h->hsums.ensure<double>((size_t)NP * H * W, h->stream);
     int* cnt = h->cnt.ensure<int>((size_t)NP, h->stream);
-    double* pk = (flags & OPOSE_OUT_DEVICE) ? peaks_out : h->hpeaks.ensure<double>((size_t)NP * 3, h->stream);
-    int* fd = (flags & OPOSE_OUT_DEVICE) ? found_out : h->hfound.ensure<int>((size_t)NP, h->stream);
+    double* pk = ((flags & OPOSE_OUT_DEVICE) ? peaks_out
+                                             : h->hpeaks.ensure<double>((size_t)(out_crop * 21 + NP) * 3, h->stream)) +
+                 (size_t)out_crop * 21 * 3;
+    int* fd = ((flags & OPOSE_OUT_DEVICE) ? found_out : h->hfound.ensure<int>((size_t)(out_crop * 21 + NP), h->stream)) +
+              (size_t)out_crop * 21;
     OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * NP, h->stream));
     h->prof_begin(pe, "gauss_threshold", 0, (double)NP * H * W * 12);
     launch_gauss_threshold(avg, NP, H, W, p.thre_hand, lab, cnt, h->stream);
@@ -1049,6 +1056,58 @@ int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
             hand_post_common(h, N, H, W, gs, p, peaks, found, flags & OPOSE_OUT_DEVICE);
         });
         hand_finish(h, N, peaks, found, flags & OPOSE_OUT_DEVICE);
+    });
+    return OPOSE_OK;
+}
+
+int opose_hand_infer_crops(opose_t* h, const uint8_t* const* crops, const int* sizes, const int64_t* row_strides,
+                           int n, const opose_params* pp, double* peaks, int32_t* found, int flags) {
+    if (!h || !crops || !sizes || !row_strides || !peaks || !found || n <= 0) return OPOSE_E_ARG;
+    for (int i = 0; i < n; ++i)
+        if (!crops[i] || sizes[i] <= 0 || row_strides[i] < (int64_t)sizes[i] * 3) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const opose_params p = fill_params(pp, OPOSE_NET_HAND);
+        const int ns = p.n_scales;
+        // per-crop geometry; the network side (Hs, Ws, Hp, Wp per scale) must agree across crops
+        std::vector<std::vector<ScaleGeom>> gs(n);
+        for (int i = 0; i < n; ++i)
+            for (int s = 0; s < ns; ++s) gs[i].push_back(geom(p.scales[s], p, sizes[i], sizes[i]));
+        for (int i = 1; i < n; ++i)
+            for (int s = 0; s < ns; ++s)
+                if (gs[i][s].Hs != gs[0][s].Hs || gs[i][s].Ws != gs[0][s].Ws)
+                    throw std::invalid_argument("crops do not share the network input size of a scale");
+        // stage the crops (host -> one device buffer)
+        std::vector<size_t> off(n + 1, 0);
+        for (int i = 0; i < n; ++i) off[i + 1] = off[i] + (size_t)row_strides[i] * sizes[i];
+        const uint8_t* base = nullptr;
+        uint8_t* buf = nullptr;
+        if (!(flags & OPOSE_IN_DEVICE)) {
+            buf = h->frames.ensure<uint8_t>(off[n], h->stream);
+            for (int i = 0; i < n; ++i)
+                OPOSE_HIP_CHECK(hipMemcpyAsync(buf + off[i], crops[i], off[i + 1] - off[i], hipMemcpyHostToDevice,
+                                               h->stream));
+        }
+        for (int s = 0; s < ns; ++s) {
+            const ScaleGeom& g0 = gs[0][s];
+            float* x = h->x.ensure<float>((size_t)n * 3 * g0.Hp * g0.Wp, h->stream);
+            ProfEntry pe;
+            h->prof_begin(pe, "preprocess", 0, 0);
+            for (int i = 0; i < n; ++i) {
+                const ScaleGeom& g = gs[i][s];
+                const uint8_t* src = buf ? buf + off[i] : crops[i];
+                launch_preprocess(src, (int64_t)(off[i + 1] - off[i]), row_strides[i], 1, sizes[i], sizes[i], g.Hs,
+                                  g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp, g.Wp, (float)p.pad_value / 256.f - 0.5f,
+                                  x + (size_t)i * 3 * g.Hp * g.Wp, h->stream);
+            }
+            h->prof_end(pe);
+            float* Sb = hand_net(h, x, n, g0.Hp, g0.Wp);
+            upsample_to_mid(h, s, Sb, 150, n, g0, 21);
+        }
+        (void)base;
+        for (int i = 0; i < n; ++i)
+            hand_post_common(h, 1, sizes[i], sizes[i], gs[i], p, peaks, found, flags & OPOSE_OUT_DEVICE, i, i);
+        hand_finish(h, n, peaks, found, flags & OPOSE_OUT_DEVICE);
     });
     return OPOSE_OK;
 }

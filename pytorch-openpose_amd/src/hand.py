@@ -66,6 +66,29 @@ class Hand(object):
                                                        self.params, peaks.ctypes.data, found.ctypes.data, 0))
         return [_as_reference_array(peaks[i], found[i]) for i in range(N)]
 
+    def batch_crops(self, crops):
+        """Square crops of different sizes (e.g. all hands util.handDetect found in a batch of
+        frames) -> list of [21, 3] arrays; the network runs once per scale for all of them."""
+        crops = [np.asarray(c) for c in crops]
+        if not crops:
+            return []
+        arrs = []
+        for c in crops:
+            if c.dtype != np.uint8 or c.ndim != 3 or c.shape[2] != 3 or c.shape[0] != c.shape[1]:
+                raise ValueError("expected square uint8 crops [w, w, 3]")
+            if not (c.strides[2] == 1 and c.strides[1] == 3):
+                c = np.ascontiguousarray(c)
+            arrs.append(c)
+        n = len(arrs)
+        ptrs = (C.c_void_p * n)(*[a.ctypes.data for a in arrs])
+        sizes = np.array([a.shape[0] for a in arrs], np.int32)
+        strides = np.array([a.strides[0] for a in arrs], np.int64)
+        peaks = np.empty((n, 21, 3), np.float64)
+        found = np.empty((n, 21), np.int32)
+        self.handle.check(_native.lib.opose_hand_infer_crops(self.handle.h, ptrs, sizes.ctypes.data, strides.ctypes.data,
+                                                             n, self.params, peaks.ctypes.data, found.ctypes.data, 0))
+        return [_as_reference_array(peaks[i], found[i]) for i in range(n)]
+
     def post(self, maps, pads, H, W):
         """Post-network path only (src/hand.py:51-75).
 

@@ -47,3 +47,44 @@ def motion_data_every_frame(body, hand, oriImg, mode: str = "body") -> np.ndarra
     if mode != "bodyhand":
         pose = pose[:18, :]
     return pose
+
+
+def motion_data_frames(body, hand, frames, mode: str = "bodyhand") -> np.ndarray:
+    """Batched `motion_data_every_frame` over equal-size frames [T, H, W, 3]: one Body launch
+    sequence for all frames, then every selected hand of every frame in one crop-batched Hand
+    launch per scale (SURVEY §8 f rank 1).  Returns [T, 60, 3] ("bodyhand") or [T, 18, 3]."""
+    frames = np.asarray(frames)
+    results = body.batch(frames)
+    T = len(frames)
+    poses = np.zeros((T, 60, 3))
+    jobs = []  # (frame, crop, x0, y0, w, is_left)
+    for t, (candidate, subset) in enumerate(results):
+        subset = subset.copy()
+        best = None
+        if len(subset) >= 1:
+            shoulder_x = np.array([candidate[int(subset[q][5])][0] for q in range(len(subset))])
+            best = np.argmax(shoulder_x)
+        if best is not None:
+            for part in range(18):
+                idx = int(subset[best][part])
+                if idx != -1:
+                    poses[t, part, :] = candidate[idx][:3]
+        for i in range(len(subset)):
+            if i != best:
+                subset[i, :] = -1
+        if mode == "bodyhand":
+            for x, y, w, is_left in util.handDetect(candidate, subset, frames[t]):
+                crop = frames[t][y:y + w, x:x + w, :]
+                jobs.append((t, np.ascontiguousarray(crop[:, ::-1]) if is_left else crop, x, y, w, is_left))
+    if jobs:
+        peaks_all = hand.batch_crops([j[1] for j in jobs])
+        for (t, _, x, y, w, is_left), peaks in zip(jobs, peaks_all):
+            if is_left:
+                peaks[:, 0] = np.where(peaks[:, 0] == 0, peaks[:, 0], w - peaks[:, 0] - 1 + x)
+                peaks[:, 1] = np.where(peaks[:, 1] == 0, peaks[:, 1], peaks[:, 1] + y)
+                poses[t, 18:39, :] = peaks
+            else:
+                peaks[:, 0] = np.where(peaks[:, 0] == 0, peaks[:, 0], peaks[:, 0] + x)
+                peaks[:, 1] = np.where(peaks[:, 1] == 0, peaks[:, 1], peaks[:, 1] + y)
+                poses[t, 39:60, :] = peaks
+    return poses if mode == "bodyhand" else poses[:, :18, :]

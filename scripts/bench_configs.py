@@ -67,6 +67,20 @@ def main():
         n_hands.append(int((pose[18:39, 2] > 0).any()) + int((pose[39:60, 2] > 0).any()))
     out["C3_bodyhand_frame_ms"] = timed(pipe, 10)
     out["C3_note"] = "hands found per frame (median over runs): %d" % int(np.median(n_hands))
+    crop2 = rng.integers(0, 256, (256, 256, 3), dtype=np.uint8)
+    out["C3_hand_two_crops_sequential_ms"] = timed(lambda: (hand(crop), hand(crop2)), 5)
+    out["C3_hand_two_crops_batched_ms"] = timed(lambda: hand.batch_crops([crop, crop2]), 5)
+    from src.pipeline import motion_data_frames
+    T = 8
+    vid = rng.integers(0, 256, (T, 368, 656, 3), dtype=np.uint8)
+    hands = []
+
+    def pipe_batch():
+        poses = motion_data_frames(body, hand, vid)
+        hands.append(int((poses[:, 18:39, 2] > 0).any(1).sum() + (poses[:, 39:60, 2] > 0).any(1).sum()))
+    ms = timed(pipe_batch, 3, warm=1)
+    out["C3_bodyhand_batched_8frames_ms_per_frame"] = ms / T
+    out["C3_bodyhand_batched_hands_per_8frames"] = int(np.median(hands))
 
     # C5
     # The 368x656 calibration carpets some heat channels at 1080p / 4 scales (plateaus above

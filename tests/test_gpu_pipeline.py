@@ -64,3 +64,32 @@ def test_body_hand_pipeline_vs_oracle(nets):
     assert got.shape == ref.shape == (60, 3)
     assert np.array_equal(got[:, :2], ref[:, :2])
     np.testing.assert_allclose(got[:, 2], ref[:, 2], rtol=1e-3, atol=1e-4)
+
+
+def test_hand_batch_crops_matches_single(nets):
+    _, hsd, _, Hand = nets
+    hand = Hand(hsd)
+    rng = np.random.default_rng(41)
+    crops = [rng.integers(0, 256, (w, w, 3), dtype=np.uint8) for w in (40, 57, 96, 128)]
+    crops.append(np.ascontiguousarray(crops[2][:, ::-1]))  # flipped left hand
+    crops.append(rng.integers(0, 256, (80, 80, 3), dtype=np.uint8)[10:60, 5:55])  # strided view
+    batch = hand.batch_crops(crops)
+    for c, b in zip(crops, batch):
+        single = hand(np.ascontiguousarray(c))
+        assert b.dtype == single.dtype and b.shape == (21, 3)
+        np.testing.assert_allclose(b, single, rtol=1e-4, atol=1e-5)
+
+
+def test_pipeline_frames_matches_per_frame(nets):
+    from src.pipeline import motion_data_every_frame, motion_data_frames
+    from src.weights import BENCH_OUT_SCALE, seeded_state_dict
+    _, hsd, Body, Hand = nets
+    body = Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE))
+    hand = Hand(hsd)
+    frames = np.random.default_rng(51).integers(0, 256, (3, 184, 240, 3), dtype=np.uint8)
+    got = motion_data_frames(body, hand, frames)
+    ref = np.stack([motion_data_every_frame(body, hand, f, mode="bodyhand") for f in frames])
+    assert got.shape == ref.shape == (3, 60, 3)
+    assert (ref[:, 18:, 2] > 0).any(), "no hand found: the test would not exercise the crop batch"
+    assert np.array_equal(got[:, :, :2], ref[:, :, :2])
+    np.testing.assert_allclose(got[:, :, 2], ref[:, :, 2], rtol=1e-3, atol=1e-4)
