@@ -93,3 +93,24 @@ def test_pipeline_frames_matches_per_frame(nets):
     assert (ref[:, 18:, 2] > 0).any(), "no hand found: the test would not exercise the crop batch"
     assert np.array_equal(got[:, :, :2], ref[:, :, :2])
     np.testing.assert_allclose(got[:, :, 2], ref[:, :, 2], rtol=1e-3, atol=1e-4)
+
+
+def test_extract_motion_data_matches_per_frame(nets, tmp_path):
+    import joblib
+    from src.motion import extract_motion_data
+    from src.pipeline import motion_data_every_frame
+    from src.weights import BENCH_OUT_SCALE, seeded_state_dict
+    _, hsd, Body, Hand = nets
+    body = Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE))
+    hand = Hand(hsd)
+    video = np.random.default_rng(61).integers(0, 256, (5, 200, 260, 3), dtype=np.uint8)
+    rec = [(10, 8), (250, 192)]  # [(x0, y0), (x1, y1)]
+    out = tmp_path / "motion.pkl"
+    got = extract_motion_data(iter(video), body, hand, outpath=str(out), recpoint=rec, mode="bodyhand", batch=2)
+    ref = np.stack([motion_data_every_frame(body, hand, f[8:192, 10:250], mode="bodyhand") for f in video])
+    assert got.shape == (5, 60, 3)
+    assert np.array_equal(got[:, :, :2], ref[:, :, :2])
+    np.testing.assert_allclose(got[:, :, 2], ref[:, :, 2], rtol=1e-3, atol=1e-4)
+    assert np.array_equal(joblib.load(out), got)
+    body_only = extract_motion_data(video, body, recpoint=rec, mode="body", batch=4)
+    assert body_only.shape == (5, 18, 3) and np.array_equal(body_only[:, :, :2], got[:, :18, :2])
