@@ -1105,6 +1105,16 @@ int opose_hand_infer_crops(opose_t* h, const uint8_t* const* crops, const int* s
             upsample_to_mid(h, s, Sb, 150, n, g0, 21);
         }
         (void)base;
+        // size every per-crop buffer for the largest crop / all crops up front: a reallocation
+        // inside the loop would drop the results of the crops already done
+        const int wmax = *std::max_element(sizes, sizes + n);
+        h->avg.ensure<double>((size_t)21 * wmax * wmax, h->stream);
+        h->hlab.ensure<int>((size_t)21 * wmax * wmax, h->stream);
+        h->hsums.ensure<double>((size_t)21 * wmax * wmax, h->stream);
+        if (!(flags & OPOSE_OUT_DEVICE)) {
+            h->hpeaks.ensure<double>((size_t)n * 21 * 3, h->stream);
+            h->hfound.ensure<int>((size_t)n * 21, h->stream);
+        }
         for (int i = 0; i < n; ++i)
             hand_post_common(h, 1, sizes[i], sizes[i], gs[i], p, peaks, found, flags & OPOSE_OUT_DEVICE, i, i);
         hand_finish(h, n, peaks, found, flags & OPOSE_OUT_DEVICE);
