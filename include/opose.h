@@ -116,6 +116,19 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W,
 int opose_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int pad_down,
                     int pad_right, int H, int W, const opose_params* p, void* records, int flags);
 
+/* Batched "fast mode" of the reference (srcmx/Batch_model.py:137-204 Batch_body.__call__):
+ * torch-bicubic pre/post-processing (inputs as transforms.ToTensor would give: uint8 / 255),
+ * single scale p->scales[0] (Batch_body: 0.5), 5x5 Gaussian + peak scores from the blurred
+ * heat map, then the same limb scoring / matching / assembly as Body.  Records as
+ * opose_body_infer. */
+int opose_batch_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride,
+                           int64_t frame_stride, const opose_params* p, void* records, int flags);
+
+/* Post-network part of the fast mode (srcmx/Batch_model.py:159-204): maps = [N,57,hl,wl]
+ * (PAF 38 | heat 19), nh x nw = int(H*s) x int(W*s) = the crop of the x8 maps, frame H x W. */
+int opose_batch_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int nh, int nw,
+                          int H, int W, const opose_params* p, void* records, int flags);
+
 /* Hand on N crops uint8 [H][W][3] (util.handDetect gives squares): peaks [N][21][3]
  * (x, y, score), found [N][21] (0 = part missing, the reference's [0,0,0] row). */
 int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride,

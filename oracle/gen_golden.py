@@ -227,3 +227,91 @@ if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "hand_detect"
     install_shims()
     sys.path.insert(0, REF)
     gen_hand_detect()
+
+
+def install_batch_shims():
+    """Extra stand-ins for srcmx/Batch_model.py + srcmx/utilmx.py imports absent here (none of
+    them is used by Batch_body.__call__): numba.jit, h5py, tslearn.metrics,
+    torchvision.transforms(.functional)."""
+    install_shims()
+    nb = types.ModuleType("numba")
+    nb.jit = lambda *a, **k: (a[0] if a and callable(a[0]) else (lambda f: f))
+    sys.modules["numba"] = nb
+    sys.modules["h5py"] = types.ModuleType("h5py")
+    tsl = types.ModuleType("tslearn")
+    tsl.metrics = types.ModuleType("tslearn.metrics")
+    sys.modules["tslearn"] = tsl
+    sys.modules["tslearn.metrics"] = tsl.metrics
+    tv = sys.modules["torchvision"]
+    tv.transforms.functional = types.ModuleType("torchvision.transforms.functional")
+    sys.modules["torchvision.transforms.functional"] = tv.transforms.functional
+    sys.path.insert(0, os.path.join(REF, "srcmx"))
+
+
+class PlantedBatch:
+    """Stand-in bodypose_model for Batch_body: fixed low-res maps per frame."""
+
+    def __init__(self, paf, heat):
+        self.paf, self.heat = torch.from_numpy(paf), torch.from_numpy(heat)
+
+    def __call__(self, x):
+        assert tuple(self.paf.shape[2:]) == (x.shape[2] // 8, x.shape[3] // 8), (self.paf.shape, x.shape)
+        return self.paf, self.heat
+
+
+def ref_batch_body(model):
+    import Batch_model as BM
+    import utilmx
+    b = BM.Batch_body.__new__(BM.Batch_body)
+    b.model = model
+    # Batch_body.__init__ (srcmx/Batch_model.py:116-135) without torch.load of the .pth
+    b.scale_search, b.boxsize, b.stride, b.padvalue, b.thre1, b.thre2 = 0.5, 368, 8, 128, 0.1, 0.05
+    b.limbSeq = [[2, 3], [2, 6], [3, 4], [4, 5], [6, 7], [7, 8], [2, 9], [9, 10], [10, 11], [2, 12], [12, 13],
+                 [13, 14], [2, 1], [1, 15], [15, 17], [1, 16], [16, 18], [3, 17], [6, 18]]
+    b.mapIdx = [[31, 32], [39, 40], [33, 34], [35, 36], [41, 42], [43, 44], [19, 20], [21, 22], [23, 24], [25, 26],
+                [27, 28], [29, 30], [47, 48], [49, 50], [53, 54], [51, 52], [55, 56], [37, 38], [45, 46]]
+    b.guassian_filter_conv = utilmx.GaussianBlurConv(19)
+    return b
+
+
+def gen_batch_body():
+    """Batch_body (srcmx/Batch_model.py:137-204) on planted maps and with the seeded network."""
+    from oracle.batch_post import size_pad, to_tensor
+    from src.model import bodypose_model
+    for seed, hw, B, n_people in ((700, (368, 656), 3, 6), (701, (240, 320), 2, 3), (702, (100, 180), 2, 2)):
+        rng = np.random.default_rng(seed)
+        H, W = hw
+        _, nh, nw, ph, pw = size_pad(0.5, H, W)
+        h, w = (nh + ph) // 8, (nw + pw) // 8
+        pafs, heats = [], []
+        for _ in range(B):
+            people, vis = planted.random_people(rng, n_people, h, w)
+            paf, heat = planted.render_body(h, w, people, vis, rng)
+            pafs.append(paf)
+            heats.append(heat)
+        paf, heat = np.stack(pafs), np.stack(heats)
+        frames = rng.integers(0, 256, (B, H, W, 3), dtype=np.uint8)
+        res = ref_batch_body(PlantedBatch(paf, heat))(to_tensor(frames))
+        d = dict(img_hw=np.array(hw), paf=paf, heat=heat)
+        for i, (c, sset) in enumerate(res):
+            d[f"candidate{i}"], d[f"subset{i}"] = np.asarray(c, np.float64), np.asarray(sset, np.float64)
+        name = f"batch_body_planted_{seed}_{H}x{W}_b{B}.npz"
+        np.savez_compressed(os.path.join(OUT, name), **d)
+        print("wrote", name, [r[0].shape for r in res], [r[1].shape for r in res])
+    m = bodypose_model().eval()
+    sd = onet.seeded_state_dict("body", 0)
+    m.load_state_dict({k: sd[".".join(k.split(".")[1:])] for k in m.state_dict().keys()})
+    frames = np.random.default_rng(23).integers(0, 256, (2, 96, 128, 3), dtype=np.uint8)
+    res = ref_batch_body(m)(to_tensor(frames))
+    d = dict(frames=frames)
+    for i, (c, sset) in enumerate(res):
+        d[f"candidate{i}"], d[f"subset{i}"] = np.asarray(c, np.float64), np.asarray(sset, np.float64)
+    np.savez_compressed(os.path.join(OUT, "batch_body_e2e_23_96x128_b2.npz"), **d)
+    print("wrote batch_body_e2e", [r[0].shape for r in res], [r[1].shape for r in res])
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "batch":
+    install_batch_shims()
+    sys.path.insert(0, REF)
+    torch.set_num_threads(8)
+    gen_batch_body()

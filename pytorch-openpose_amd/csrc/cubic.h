@@ -40,6 +40,39 @@ __device__ __forceinline__ CubicTap cubic_tap(int d, double scale, int ssize) {
     return t;
 }
 
+// PyTorch upsample_bicubic2d (align_corners=False, A = -0.75; aten UpSample.h): source
+// coordinate scale * (d + 0.5) - 0.5 in float (scale = float(1 / scale_factor), or
+// float(in) / float(out) when a size is given), index clamped to the last row, lambda clamped
+// to [0, 1], each of the four coefficients from its own polynomial (no 1 - sum), taps clamped.
+// Used by the Batch_body fast mode (srcmx/Batch_model.py:147-168).
+__device__ __forceinline__ CubicTap cubic_tap_torch(int d, float scale, int ssize) {
+    CubicTap t;
+    const float A = -0.75f;
+    const float real = scale * ((float)d + 0.5f) - 0.5f;
+    int idx = (int)floorf(real);
+    idx = idx < ssize - 1 ? idx : ssize - 1;
+    float lam = real - (float)idx;
+    lam = fminf(fmaxf(lam, 0.f), 1.f);
+    const float x1 = lam + 1.f;
+    t.c[0] = ((A * x1 - 5.f * A) * x1 + 8.f * A) * x1 - 4.f * A;
+    t.c[1] = ((A + 2.f) * lam - (A + 3.f)) * lam * lam + 1.f;
+    const float x2 = 1.f - lam;
+    t.c[2] = ((A + 2.f) * x2 - (A + 3.f)) * x2 * x2 + 1.f;
+    const float x3 = x2 + 1.f;
+    t.c[3] = ((A * x3 - 5.f * A) * x3 + 8.f * A) * x3 - 4.f * A;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int v = idx - 1 + j;
+        t.i[j] = v < 0 ? 0 : (v >= ssize ? ssize - 1 : v);
+    }
+    return t;
+}
+
+// taps of either convention (torch: scale holds the exact float scale)
+__device__ __forceinline__ CubicTap cubic_tap_any(int d, double scale, int ssize, bool torch) {
+    return torch ? cubic_tap_torch(d, (float)scale, ssize) : cubic_tap(d, scale, ssize);
+}
+
 // float32 image: horizontal then vertical pass, ((p0+p1)+p2)+p3 each.
 // plane: row-major [rows][ld] (ld = row stride in floats)
 __device__ __forceinline__ float cubic_sample_f32(const float* __restrict__ plane, int ld, const CubicTap& ty,

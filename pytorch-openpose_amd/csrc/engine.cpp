@@ -671,6 +671,60 @@ static int worst_status(const uint8_t* rec, int N, size_t bytes) {
         return OPOSE_E_WEIGHTS;                \
     }
 
+// Batch_body fast mode after the network (srcmx/Batch_model.py:159-204): torch bicubic x8
+// cropped to nh x nw, torch bicubic to H x W, 5x5 blur + peaks on the blurred map, then the
+// shared limb scoring / greedy matching / assembly.  maps: [N][cstride][hl][wl] with PAF
+// channels 0..37 and heat 38..56.
+static void batch_post_common(opose_ctx* h, int N, int H, int W, const float* maps, int cstride, int hl, int wl,
+                              int nh, int nw, const opose_params& p, uint8_t* rec_dev) {
+    const RecordLayout L = make_record_layout(h->ppp, h->maxp);
+    const int cap = h->ppp;
+    ProfEntry pe;
+    float* mid = h->mids[0].ensure<float>((size_t)N * 56 * nh * nw, h->stream);
+    h->prof_begin(pe, "upsample8", 0, (double)N * 56 * nh * nw * 4);
+    launch_upsample8_torch(maps, cstride, 0, 56, N, hl, wl, nh, nw, mid, h->stream);
+    h->prof_end(pe);
+    float* heat = reinterpret_cast<float*>(h->avg.ensure<double>((size_t)N * 18 * H * W, h->stream));
+    h->prof_begin(pe, "heat_full", 0, (double)N * 18 * (4.0 * H * W + 4.0 * nh * nw));
+    launch_resize_torch_f32(mid, 56, 38, 18, N, nh, nw, H, W, heat, h->stream);
+    h->prof_end(pe);
+    PafScales S{};
+    S.mid[0] = mid;
+    S.hs[0] = nh;
+    S.ws[0] = nw;
+    S.sy[0] = (double)((float)nh / (float)H);
+    S.sx[0] = (double)((float)nw / (float)W);
+    S.n = 1;
+    S.cm = 56;
+    S.H = H;
+    S.W = W;
+    S.torch = 1;
+    int* cnt = h->cnt.ensure<int>((size_t)N * 18, h->stream);
+    int* list = h->list.ensure<int>((size_t)N * 18 * cap, h->stream);
+    double* lscore = h->list_score.ensure<double>((size_t)N * 18 * cap, h->stream);
+    int* pos = h->peak_pos.ensure<int>((size_t)N * 18 * cap, h->stream);
+    int* pcnt = h->part_cnt.ensure<int>((size_t)N * 18, h->stream);
+    double* score = h->score.ensure<double>((size_t)N * 19 * cap * cap, h->stream);
+    Conn* conn = h->conn.ensure<Conn>((size_t)N * 19 * cap, h->stream);
+    int* ccnt = h->conn_cnt.ensure<int>((size_t)N * 19, h->stream);
+    OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * N * 18, h->stream));
+    h->prof_begin(pe, "gauss_nms", 0, (double)N * 18 * H * W * 4);
+    launch_blur5_nms(heat, N * 18, H, W, p.thre1, cap, cnt, list, lscore, h->stream);
+    h->prof_end(pe);
+    h->prof_begin(pe, "peaks_finalize", 0, 0);
+    launch_peaks_finalize(cnt, list, lscore, N, H, W, L, rec_dev, pos, pcnt, h->stream);
+    h->prof_end(pe);
+    h->prof_begin(pe, "paf_score", 0, 0);
+    launch_paf_score(S, pos, pcnt, N, cap, p.thre2, score, h->stream);
+    h->prof_end(pe);
+    h->prof_begin(pe, "limb_greedy", 0, 0);
+    launch_limb_greedy(score, pcnt, N, cap, conn, ccnt, h->stream);
+    h->prof_end(pe);
+    h->prof_begin(pe, "assemble", 0, 0);
+    launch_assemble(conn, ccnt, pcnt, N, L, rec_dev, h->stream);
+    h->prof_end(pe);
+}
+
 // Run `work` (device work only: kernels, device memsets/copies on h->stream, no host sync,
 // no allocation once warm) through the launch-sequence cache keyed by `key`.
 template <class F>
@@ -969,6 +1023,64 @@ int opose_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int pa
         uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)
                                                   : h->records.ensure<uint8_t>(L.bytes * N, h->stream);
         body_post_common(h, N, H, W, {g}, p, rec);
+        return finish_records(h, N, records, rec, flags);
+    });
+}
+
+int opose_batch_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride,
+                           int64_t frame_stride, const opose_params* pp, void* records, int flags) {
+    if (!h || !bgr || !records || N <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
+    if (row_stride < (int64_t)W * 3 || frame_stride < row_stride * H) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const opose_params p = fill_params(pp, OPOSE_NET_BODY);
+        const RecordLayout L = make_record_layout(h->ppp, h->maxp);
+        // Batch_body.calculate_size_pad (srcmx/Batch_model.py:302-307): int() truncation
+        const double scale = p.boxsize * p.scales[0] / H;
+        const int nh = (int)(H * scale), nw = (int)(W * scale);
+        if (nh <= 0 || nw <= 0) throw std::invalid_argument("scale produces an empty image");
+        const int Hp = round_up(nh, p.stride), Wp = round_up(nw, p.stride);
+        const uint8_t* fd = bgr;
+        if (!(flags & OPOSE_IN_DEVICE)) {
+            uint8_t* buf = h->frames.ensure<uint8_t>((size_t)frame_stride * N, h->stream);
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, (size_t)frame_stride * N, hipMemcpyHostToDevice, h->stream));
+            fd = buf;
+        }
+        uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)
+                                                  : h->records.ensure<uint8_t>(L.bytes * N, h->stream);
+        const std::string key = call_key("batch_body", N, H, W, row_stride, frame_stride, p, fd, rec, h->ppp, h->maxp);
+        run_graphed(h, key, [&] {
+            float* x = h->x.ensure<float>((size_t)N * 3 * Hp * Wp, h->stream);
+            ProfEntry pe;
+            h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * Hp * Wp));
+            const float sc = (float)(1.0 / scale);  // torch: float(1 / scale_factor)
+            launch_preprocess_torch(fd, frame_stride, row_stride, N, H, W, nh, nw, sc, sc, Hp, Wp, x, h->stream);
+            h->prof_end(pe);
+            float* S = body_net(h, x, N, Hp, Wp);
+            batch_post_common(h, N, H, W, S, 185, Hp / 8, Wp / 8, nh, nw, p, rec);
+        });
+        return finish_records(h, N, records, rec, flags);
+    });
+}
+
+int opose_batch_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int nh, int nw, int H, int W,
+                          const opose_params* pp, void* records, int flags) {
+    if (!h || !maps || !records || N <= 0 || hl <= 0 || wl <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
+    if (nh <= 0 || nw <= 0 || nh > 8 * hl || nw > 8 * wl) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const opose_params p = fill_params(pp, OPOSE_NET_BODY);
+        const RecordLayout L = make_record_layout(h->ppp, h->maxp);
+        const size_t n_in = (size_t)N * 57 * hl * wl;
+        const float* md = maps;
+        if (!(flags & OPOSE_IN_DEVICE)) {
+            float* buf = h->maps_in.ensure<float>(n_in, h->stream);
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, maps, n_in * 4, hipMemcpyHostToDevice, h->stream));
+            md = buf;
+        }
+        uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)
+                                                  : h->records.ensure<uint8_t>(L.bytes * N, h->stream);
+        batch_post_common(h, N, H, W, md, 57, hl, wl, nh, nw, p, rec);
         return finish_records(h, N, records, rec, flags);
     });
 }

@@ -9,6 +9,8 @@
 //  * src/body.py:57,67  cv2.resize(map, (W, H)) + heatmap_avg += map / n_scales (float64)
 //                                                         => heat_full_accum
 // Compiled with -ffp-contract=off (see cubic.h).
+#include <stdexcept>
+
 #include "common.h"
 #include "cubic.h"
 #include "kernels.h"
@@ -104,7 +106,8 @@ constexpr int RS_MAXR = 44;    // staged source rows (RT * scale + 5 <= 44  <=> 
 template <int MODE, int MAXR>
 __global__ __launch_bounds__(256) void cubic_resize_rows(const float* __restrict__ in, int in_cstride, int in_coff,
                                                          int C, int hi, int wi, int ho, int wo, double sy, double sx,
-                                                         float nscales, int accumulate, void* __restrict__ out) {
+                                                         float nscales, int accumulate, void* __restrict__ out,
+                                                         int torch) {
     __shared__ float hs[MAXR][256];
     const int tid = threadIdx.x;
     const int x = blockIdx.x * 256 + tid;
@@ -114,11 +117,11 @@ __global__ __launch_bounds__(256) void cubic_resize_rows(const float* __restrict
     const int n = nc / C, c = nc - n * C;
     const float* plane = in + ((size_t)n * in_cstride + in_coff + c) * hi * wi;
     // staged source rows: the clamped tap rows of the first and last output row bound them
-    const int r_lo = cubic_tap(y0, sy, hi).i[0];
-    const int r_hi = cubic_tap(y1 - 1, sy, hi).i[3];
+    const int r_lo = cubic_tap_any(y0, sy, hi, torch).i[0];
+    const int r_hi = cubic_tap_any(y1 - 1, sy, hi, torch).i[3];
     const bool live = x < wo;
     if (live) {
-        const CubicTap tx = cubic_tap(x, sx, wi);
+        const CubicTap tx = cubic_tap_any(x, sx, wi, torch);
         for (int r = r_lo; r <= r_hi; ++r) {
             const float* row = plane + (size_t)r * wi;
             float v = row[tx.i[0]] * tx.c[0];
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(256) void cubic_resize_rows(const float* __restrict
     __syncthreads();
     if (!live) return;
     for (int y = y0; y < y1; ++y) {
-        const CubicTap ty = cubic_tap(y, sy, hi);
+        const CubicTap ty = cubic_tap_any(y, sy, hi, torch);
         float o = hs[ty.i[0] - r_lo][tid] * ty.c[0];
         o = o + hs[ty.i[1] - r_lo][tid] * ty.c[1];
         o = o + hs[ty.i[2] - r_lo][tid] * ty.c[2];
@@ -154,17 +157,18 @@ static bool rows_fit(double scale) { return RS_RT * scale + 5.0 <= (double)RS_MA
 
 template <int MODE>
 static void launch_resize_rows(dim3 grid, hipStream_t st, const float* in, int cstride, int coff, int C, int hi,
-                               int wi, int ho, int wo, double sy, double sx, float ns, int acc, void* out) {
+                               int wi, int ho, int wo, double sy, double sx, float ns, int acc, void* out,
+                               int torch = 0) {
     const double need = RS_RT * sy + 5.0;
     if (need <= 8.0)
         hipLaunchKernelGGL((cubic_resize_rows<MODE, 8>), grid, dim3(256), 0, st, in, cstride, coff, C, hi, wi, ho, wo,
-                           sy, sx, ns, acc, out);
+                           sy, sx, ns, acc, out, torch);
     else if (need <= 16.0)
         hipLaunchKernelGGL((cubic_resize_rows<MODE, 16>), grid, dim3(256), 0, st, in, cstride, coff, C, hi, wi, ho,
-                           wo, sy, sx, ns, acc, out);
+                           wo, sy, sx, ns, acc, out, torch);
     else
         hipLaunchKernelGGL((cubic_resize_rows<MODE, RS_MAXR>), grid, dim3(256), 0, st, in, cstride, coff, C, hi, wi,
-                           ho, wo, sy, sx, ns, acc, out);
+                           ho, wo, sy, sx, ns, acc, out, torch);
 }
 
 void launch_preprocess(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int Hs,
@@ -202,6 +206,72 @@ void launch_heat_full_f32(const float* mid, int Cm, int coff, int P, int N, int 
     dim3 grid((W + 255) / 256, H, N * P);
     hipLaunchKernelGGL(heat_full_accum<float>, grid, dim3(256), 0, st, mid, Cm, coff, P, Hs, Ws, H, W, sy, sx, 1.f, 0,
                        avg);
+}
+
+// ---------------------------------------------------------------- Batch_body fast mode
+// transforms.ToTensor (uint8 / 255.f) -> F.interpolate(bicubic, scale_factor) -> - 0.5 ->
+// F.pad(0) on the right / bottom (srcmx/Batch_model.py:147-150): torch bicubic taps in float,
+// rows first, x0*c0 + x1*c1 + x2*c2 + x3*c3.
+__global__ __launch_bounds__(256) void preprocess_torch_u8(const uint8_t* __restrict__ src, int64_t frame_stride,
+                                                           int64_t row_stride, int H, int W, int nh, int nw,
+                                                           float scale_y, float scale_x, int Hp, int Wp,
+                                                           float* __restrict__ out) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int n = blockIdx.z;
+    if (x >= Wp) return;
+    const size_t plane = (size_t)Hp * Wp;
+    float* o = out + (size_t)n * 3 * plane + (size_t)y * Wp + x;
+    if (y >= nh || x >= nw) {
+        o[0] = 0.f;
+        o[plane] = 0.f;
+        o[2 * plane] = 0.f;
+        return;
+    }
+    const CubicTap ty = cubic_tap_torch(y, scale_y, H);
+    const CubicTap tx = cubic_tap_torch(x, scale_x, W);
+    const uint8_t* f = src + (size_t)n * frame_stride;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float h[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint8_t* row = f + (size_t)ty.i[r] * row_stride;
+            float v = (float)row[3 * tx.i[0] + c] / 255.f * tx.c[0];
+            v = v + (float)row[3 * tx.i[1] + c] / 255.f * tx.c[1];
+            v = v + (float)row[3 * tx.i[2] + c] / 255.f * tx.c[2];
+            v = v + (float)row[3 * tx.i[3] + c] / 255.f * tx.c[3];
+            h[r] = v;
+        }
+        float v = h[0] * ty.c[0];
+        v = v + h[1] * ty.c[1];
+        v = v + h[2] * ty.c[2];
+        v = v + h[3] * ty.c[3];
+        o[(size_t)c * plane] = v - 0.5f;
+    }
+}
+
+void launch_preprocess_torch(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int nh,
+                             int nw, float scale_y, float scale_x, int Hp, int Wp, float* out, hipStream_t st) {
+    dim3 grid((Wp + 255) / 256, Hp, N);
+    hipLaunchKernelGGL(preprocess_torch_u8, grid, dim3(256), 0, st, src, frame_stride, row_stride, H, W, nh, nw,
+                       scale_y, scale_x, Hp, Wp, out);
+}
+
+// torch bicubic x8 of channels [in_coff, in_coff + C) cropped to nh x nw (scale 1/8 exactly)
+void launch_upsample8_torch(const float* in, int in_cstride, int in_coff, int C, int N, int hl, int wl, int nh, int nw,
+                            float* out, hipStream_t st) {
+    dim3 grid((nw + 255) / 256, (nh + RS_RT - 1) / RS_RT, N * C);
+    launch_resize_rows<0>(grid, st, in, in_cstride, in_coff, C, hl, wl, nh, nw, 0.125, 0.125, 1.f, 0, (void*)out, 1);
+}
+
+// torch bicubic to H x W (size given: scale = float(nh) / float(H)); float map out
+void launch_resize_torch_f32(const float* mid, int Cm, int coff, int P, int N, int nh, int nw, int H, int W,
+                             float* out, hipStream_t st) {
+    const float sy = (float)nh / (float)H, sx = (float)nw / (float)W;
+    if (!rows_fit(sy)) throw std::invalid_argument("fast mode: downscale too strong for the staged resize");
+    dim3 grid((W + 255) / 256, (H + RS_RT - 1) / RS_RT, N * P);
+    launch_resize_rows<1>(grid, st, mid, Cm, coff, P, nh, nw, H, W, (double)sy, (double)sx, 1.f, 0, (void*)out, 1);
 }
 
 }  // namespace opose

@@ -12,6 +12,7 @@ struct PafScales {
     int hs[kMaxScales], ws[kMaxScales];
     double sy[kMaxScales], sx[kMaxScales];  // source step of the final resize to H x W
     int n, cm, H, W;
+    int torch;  // 1: torch bicubic taps (Batch_body fast mode), 0: OpenCV INTER_CUBIC
 };
 
 struct Conn {
@@ -38,8 +39,20 @@ void launch_heat_full(const float* mid, int Cm, int coff, int P, int N, int Hs, 
 void launch_heat_full_f32(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
                           double sx, float* avg, hipStream_t st);
 
+// Batch_body fast mode (torch bicubic conventions)
+void launch_preprocess_torch(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int nh,
+                             int nw, float scale_y, float scale_x, int Hp, int Wp, float* out, hipStream_t st);
+void launch_upsample8_torch(const float* in, int in_cstride, int in_coff, int C, int N, int hl, int wl, int nh, int nw,
+                            float* out, hipStream_t st);
+void launch_resize_torch_f32(const float* mid, int Cm, int coff, int P, int N, int nh, int nw, int H, int W,
+                             float* out, hipStream_t st);
+
 // post.hip
 void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
+                      double* list_score, hipStream_t st);
+// Batch_body fast mode: 5x5 Gaussian (reflect pad, srcmx/utilmx.py:246-263) + findpeaks_torch
+// (srcmx/utilmx.py:230-243) on heat [NP][H][W] float; scores = blurred values
+void launch_blur5_nms(const float* heat, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
                       double* list_score, hipStream_t st);
 void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st);
 void launch_peaks_finalize(const int* cnt, const int* list, const double* list_score, int N, int H, int W,

@@ -168,6 +168,75 @@ __global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict_
     if (threadIdx.x == 0 && s_n) atomicAdd(cnt + np, s_n);
 }
 
+// ---------------------------------------------------------------- Batch_body fast mode
+// srcmx/utilmx.py:251-255 (float32)
+__constant__ float kBlur5[5][5] = {{0.00078633f, 0.00655965f, 0.01330373f, 0.00655965f, 0.00078633f},
+                                   {0.00655965f, 0.05472157f, 0.11098164f, 0.05472157f, 0.00655965f},
+                                   {0.01330373f, 0.11098164f, 0.22508352f, 0.11098164f, 0.01330373f},
+                                   {0.00655965f, 0.05472157f, 0.11098164f, 0.05472157f, 0.00655965f},
+                                   {0.00078633f, 0.00655965f, 0.01330373f, 0.00655965f, 0.00078633f}};
+
+// torch 'reflect' padding: edge not repeated (d c b | a b c d | c b a)
+__device__ __forceinline__ int reflect101(int i, int n) {
+    if (n == 1) return 0;
+    const int p = 2 * n - 2;
+    i %= p;
+    if (i < 0) i += p;
+    return i < n ? i : p - i;
+}
+
+constexpr int BT = 32;            // output tile (BT x BT)
+constexpr int BI = BT + 6;        // input tile: 2 (blur) + 1 (NMS ring) each side
+
+// heat [NP][H][W] float; one workgroup per BT x BT tile of one part map (1-D XCD-ordered grid)
+__global__ __launch_bounds__(256) void blur5_nms(const float* __restrict__ heat, int H, int W, double thre, int cap,
+                                                 int* __restrict__ cnt, int* __restrict__ list,
+                                                 double* __restrict__ list_score) {
+    __shared__ float s_in[BI][BI];
+    __shared__ float s_b[BT + 2][BT + 2];
+    const int ntx = (W + BT - 1) / BT, nty = (H + BT - 1) / BT;
+    const int total = gridDim.x, b = blockIdx.x;
+    const int q = total >> 3, rr = total & 7, xcd = b & 7;
+    const int id = xcd * q + min(xcd, rr) + (b >> 3);
+    const int tx = id % ntx, rest = id / ntx;
+    const int ty = rest % nty, np = rest / nty;
+    const int x0 = tx * BT, y0 = ty * BT;
+    const float* m = heat + (size_t)np * H * W;
+    for (int e = threadIdx.x; e < BI * BI; e += 256) {
+        const int r = e / BI, c = e - r * BI;
+        s_in[r][c] = m[(size_t)reflect101(y0 - 3 + r, H) * W + reflect101(x0 - 3 + c, W)];
+    }
+    __syncthreads();
+    // blurred values for the tile plus a 1-pixel ring (rows / cols y0-1 .. y0+BT)
+    for (int e = threadIdx.x; e < (BT + 2) * (BT + 2); e += 256) {
+        const int r = e / (BT + 2), c = e - r * (BT + 2);
+        float acc = 0.f;
+#pragma unroll
+        for (int dy = 0; dy < 5; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 5; ++dx) acc = acc + s_in[r + dy][c + dx] * kBlur5[dy][dx];
+        s_b[r][c] = acc;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < BT * BT; e += 256) {
+        const int r = e / BT, c = e - r * BT;
+        const int y = y0 + r, x = x0 + c;
+        if (y >= H || x >= W) continue;
+        const float v = s_b[r + 1][c + 1];
+        const float up = y > 0 ? s_b[r][c + 1] : 0.f;     // findpeaks_torch pads with zeros
+        const float dn = y < H - 1 ? s_b[r + 2][c + 1] : 0.f;
+        const float lf = x > 0 ? s_b[r + 1][c] : 0.f;
+        const float rt = x < W - 1 ? s_b[r + 1][c + 2] : 0.f;
+        if (v > (float)thre && v >= up && v >= dn && v >= lf && v >= rt) {
+            const int slot = atomicAdd(cnt + np, 1);
+            if (slot < cap) {
+                list[(size_t)np * cap + slot] = y * W + x;
+                list_score[(size_t)np * cap + slot] = (double)v;  // the blurred value (Batch_model.py:191)
+            }
+        }
+    }
+}
+
 // One workgroup per frame: order each part's peaks row-major (np.nonzero), assign the
 // global running ids, write candidate rows (x, y, score, id) into the record.
 __global__ __launch_bounds__(256) void peaks_finalize(const int* __restrict__ cnt, const int* __restrict__ list,
@@ -259,8 +328,8 @@ __global__ __launch_bounds__(256) void paf_score(PafScales S, const int* __restr
                     vx_ = mx[(size_t)Y * S.ws[s] + X];
                     vy_ = mx[plane + (size_t)Y * S.ws[s] + X];
                 } else {
-                    const CubicTap ty = cubic_tap(Y, S.sy[s], S.hs[s]);
-                    const CubicTap tx = cubic_tap(X, S.sx[s], S.ws[s]);
+                    const CubicTap ty = cubic_tap_any(Y, S.sy[s], S.hs[s], S.torch);
+                    const CubicTap tx = cubic_tap_any(X, S.sx[s], S.ws[s], S.torch);
                     vx_ = cubic_sample_f32(mx, S.ws[s], ty, tx);
                     vy_ = cubic_sample_f32(mx + plane, S.ws[s], ty, tx);
                 }
@@ -468,6 +537,12 @@ void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double th
     else
         hipLaunchKernelGGL(gauss_nms<double>, grid, dim3(256), 0, st, (const double*)avg, 18, H, W, thre, cap, cnt,
                            list, list_score);
+}
+
+void launch_blur5_nms(const float* heat, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
+                      double* list_score, hipStream_t st) {
+    dim3 grid(((W + BT - 1) / BT) * ((H + BT - 1) / BT) * NP);
+    hipLaunchKernelGGL(blur5_nms, grid, dim3(256), 0, st, heat, H, W, thre, cap, cnt, list, list_score);
 }
 
 void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st) {

@@ -82,6 +82,19 @@ def main():
     out["C3_bodyhand_batched_8frames_ms_per_frame"] = ms / T
     out["C3_bodyhand_batched_hands_per_8frames"] = int(np.median(hands))
 
+    # fast mode (srcmx/Batch_model.py Batch_body) on the C4 batch: 32 frames 368x656 per GPU
+    from src.batch_model import Batch_body
+    bb = Batch_body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE), peaks_per_part=256, max_people=128)
+    f32 = torch.from_numpy(rng.integers(0, 256, (32, 368, 656, 3), dtype=np.uint8)).to(dev)
+    recb = torch.empty((32, bb.handle.record_bytes()), dtype=torch.uint8, device=dev)
+
+    def stepb():
+        bb.infer_records(f32, recb)
+        bb.handle.synchronize()
+    ms = timed(stepb, 5, warm=2)
+    out["fast_mode_batch_body_frames_per_s"] = 32 / (ms * 1e-3)
+    out["fast_mode_status_nonzero"] = int((recb.view(torch.int32)[:, 0] != 0).sum().item())
+
     # C5
     # The 368x656 calibration carpets some heat channels at 1080p / 4 scales (plateaus above
     # thre1); a -3.5 shift of the heat biases gives ~1-10 peaks per part (scripts/calib_c5.py).

@@ -107,3 +107,37 @@ def test_flops_match_survey():
     assert network.body_flops(184, 328) == 121158571264
     assert network.body_flops(184, 184) == 67967003392
     assert network.hand_flops(368, 368) == 206375342080
+
+
+# ---- Batch_body fast mode (srcmx/Batch_model.py:137-204) ---------------------------------
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "batch_body_planted_*.npz"))),
+                         ids=os.path.basename)
+def test_batch_oracle_planted_matches_reference(path):
+    import torch
+    from oracle import batch_post
+    d = np.load(path)
+    H, W = (int(v) for v in d["img_hw"])
+    _, nh, nw, _, _ = batch_post.size_pad(0.5, H, W)
+    res = batch_post.post(torch.from_numpy(d["paf"]), torch.from_numpy(d["heat"]), (H, W, nh, nw))
+    for i, (c, s) in enumerate(res):
+        assert np.array_equal(np.asarray(c, np.float64).reshape(-1, 4) if len(c) else c, d[f"candidate{i}"])
+        assert np.array_equal(s, d[f"subset{i}"])
+
+
+def test_batch_oracle_e2e_matches_reference():
+    import torch
+    from oracle import batch_post, network
+    d = np.load(os.path.join(GOLDEN, "batch_body_e2e_23_96x128_b2.npz"))
+    sd = network.seeded_state_dict("body", 0)
+
+    def net_fn(x):
+        p, h = network.body_forward(torch.from_numpy(x), sd)
+        return p.numpy(), h.numpy()
+    res = batch_post.batch_body_infer(d["frames"], net_fn)
+    for i, (c, s) in enumerate(res):
+        ref_c, ref_s = d[f"candidate{i}"], d[f"subset{i}"]
+        # the torch-CPU network here vs the reference's nn.Module: same ops, fp32 noise only
+        assert c.shape == ref_c.shape and s.shape == ref_s.shape
+        assert np.array_equal(c[:, [0, 1, 3]], ref_c[:, [0, 1, 3]])
+        np.testing.assert_allclose(c[:, 2], ref_c[:, 2], rtol=1e-5, atol=1e-6)
+        assert np.array_equal(s[:, :18], ref_s[:, :18])
