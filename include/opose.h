@@ -129,6 +129,19 @@ int opose_batch_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, 
 int opose_batch_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int nh, int nw,
                           int H, int W, const opose_params* p, void* records, int flags);
 
+/* Fast-mode hand (srcmx/Batch_model.py:310-354 Batch_hand.__call__): N crops already resized
+ * to H x W (the data loader's boxsize, a multiple of 8) as uint8 BGR; network at scale 1,
+ * torch bicubic x8, 5x5 Gaussian, components of blurred > p->thre_hand (Batch_hand: 0.035)
+ * selected on the blurred map.  peaks [N][21][3] in the H x W frame, found [N][21]. */
+int opose_batch_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride,
+                           int64_t frame_stride, const opose_params* p, double* peaks, int32_t* found,
+                           int flags);
+
+/* Post-network part of the fast-mode hand (srcmx/Batch_model.py:334-354): maps = [N,22,hl,wl]
+ * network outputs; peaks in the (8 hl) x (8 wl) frame. */
+int opose_batch_hand_post(opose_t* h, const float* maps, int N, int hl, int wl, const opose_params* p,
+                          double* peaks, int32_t* found, int flags);
+
 /* Hand on N crops uint8 [H][W][3] (util.handDetect gives squares): peaks [N][21][3]
  * (x, y, score), found [N][21] (0 = part missing, the reference's [0,0,0] row). */
 int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride,

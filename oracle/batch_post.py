@@ -94,3 +94,32 @@ def batch_body_infer(frames_u8: np.ndarray, net_fn, g_scale=0.5, thre1=0.1, thre
     x, geo = net_input(frames_u8, g_scale)
     paf, heat = net_fn(x.numpy())
     return post(torch.from_numpy(np.asarray(paf)), torch.from_numpy(np.asarray(heat)), geo, thre1, thre2)
+
+
+def hand_post(heat_low: torch.Tensor, thre=0.035, stride=8):
+    """Batch_hand.__call__ after the network (srcmx/Batch_model.py:334-354) -> np.array [B, 21, 3]."""
+    from .hand_post import label8, npmax
+    heat = F.interpolate(heat_low, scale_factor=stride, mode="bicubic")
+    heat = blur5(heat).numpy().transpose(0, 2, 3, 1)
+    out = []
+    for i in range(heat.shape[0]):
+        peaks = []
+        for part in range(21):
+            m = heat[i, :, :, part]
+            binary = m > thre
+            if np.sum(binary) == 0:
+                peaks.append([0, 0, 0])
+                continue
+            lab, n = label8(binary)
+            best = np.argmax([np.sum(m[lab == k]) for k in range(1, n + 1)]) + 1
+            m[lab != best] = 0
+            y, x = npmax(m)
+            peaks.append([x, y, np.max(m)])
+        out.append(peaks)
+    return np.array(out)
+
+
+def batch_hand_infer(crops_u8: np.ndarray, net_fn, thre=0.035):
+    """crops already at the data loader's size; net_fn(x [B,3,h,w] numpy) -> heat numpy."""
+    x = to_tensor(crops_u8) - 0.5
+    return hand_post(torch.from_numpy(np.asarray(net_fn(x.numpy()))), thre)

@@ -310,8 +310,56 @@ def gen_batch_body():
     print("wrote batch_body_e2e", [r[0].shape for r in res], [r[1].shape for r in res])
 
 
+class PlantedHandBatch:
+    """Stand-in handpose_model for Batch_hand: fixed [B, 22, 46, 46] maps."""
+
+    def __init__(self, heat):
+        self.heat = torch.from_numpy(heat)
+
+    def __call__(self, x):
+        assert tuple(self.heat.shape[2:]) == (x.shape[2] // 8, x.shape[3] // 8)
+        return self.heat
+
+
+def ref_batch_hand(model):
+    import Batch_model as BM
+    import utilmx
+    b = BM.Batch_hand.__new__(BM.Batch_hand)
+    b.model = model
+    # Batch_hand.__init__ (srcmx/Batch_model.py:311-324) without torch.load of the .pth
+    b.scale_search, b.boxsize, b.stride, b.padValue, b.thre = [1.0], 368, 8, 128, 0.035
+    b.guassian_filter_conv = utilmx.GaussianBlurConv(22)
+    return b
+
+
+def gen_batch_hand():
+    """Batch_hand (srcmx/Batch_model.py:326-354) on planted hand maps and the seeded network."""
+    from oracle.batch_post import to_tensor
+    from src.model import handpose_model
+    rng0 = np.random.default_rng(88)
+    heats = []
+    for seed, vis_p, extra in ((800, 0.9, 0), (801, 0.7, 2), (802, 0.0, 0), (803, 1.0, 3)):
+        rng = np.random.default_rng(seed)
+        pts = rng0.uniform(0.15, 0.85, size=(21, 2))
+        vis = rng.random(21) < vis_p
+        heats.append(planted.render_hand(46, 46, pts, vis, rng, extra_blobs=extra))
+    heat = np.stack(heats)
+    crops = np.random.default_rng(9).integers(0, 256, (len(heats), 368, 368, 3), dtype=np.uint8)
+    peaks = ref_batch_hand(PlantedHandBatch(heat))(to_tensor(crops))
+    np.savez_compressed(os.path.join(OUT, "batch_hand_planted_b4.npz"), heat=heat, peaks=peaks)
+    print("wrote batch_hand_planted", peaks.dtype, peaks.shape)
+    m = handpose_model().eval()
+    sd = onet.seeded_state_dict("hand", 0)
+    m.load_state_dict({k: sd[".".join(k.split(".")[1:])] for k in m.state_dict().keys()})
+    crops = np.random.default_rng(10).integers(0, 256, (2, 64, 64, 3), dtype=np.uint8)
+    peaks = ref_batch_hand(m)(to_tensor(crops))
+    np.savez_compressed(os.path.join(OUT, "batch_hand_e2e_b2_64.npz"), crops=crops, peaks=peaks)
+    print("wrote batch_hand_e2e", peaks.dtype, peaks.shape)
+
+
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "batch":
     install_batch_shims()
     sys.path.insert(0, REF)
     torch.set_num_threads(8)
     gen_batch_body()
+    gen_batch_hand()

@@ -1172,6 +1172,78 @@ int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
     return OPOSE_OK;
 }
 
+// Batch_hand after the network (srcmx/Batch_model.py:334-354): maps [N][cstride][H/8][W/8]
+// with the 22 heat channels first
+static void batch_hand_post_common(opose_ctx* h, int N, int H, int W, const float* maps, int cstride,
+                                   const opose_params& p, double* peaks, int32_t* found, int flags) {
+    const int NP = N * 21;
+    ProfEntry pe;
+    float* mid = h->mids[0].ensure<float>((size_t)NP * H * W, h->stream);
+    h->prof_begin(pe, "upsample8", 0, (double)NP * H * W * 4);
+    launch_upsample8_torch(maps, cstride, 0, 21, N, H / 8, W / 8, H, W, mid, h->stream);
+    h->prof_end(pe);
+    double* avg = h->avg.ensure<double>((size_t)NP * H * W, h->stream);
+    int* lab = h->hlab.ensure<int>((size_t)NP * H * W, h->stream);
+    double* sums = h->hsums.ensure<double>((size_t)NP * H * W, h->stream);
+    int* cnt = h->cnt.ensure<int>((size_t)NP, h->stream);
+    const bool od = flags & OPOSE_OUT_DEVICE;
+    double* pk = od ? peaks : h->hpeaks.ensure<double>((size_t)NP * 3, h->stream);
+    int* fo = od ? found : h->hfound.ensure<int>((size_t)NP, h->stream);
+    OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * NP, h->stream));
+    h->prof_begin(pe, "gauss_threshold", 0, (double)NP * H * W * 16);
+    launch_blur5_seed(mid, NP, H, W, p.thre_hand, avg, lab, cnt, h->stream);
+    h->prof_end(pe);
+    h->prof_begin(pe, "hand_cc", 0, 0);
+    void* ws = h->hsel.ensure<uint8_t>(hand_cc_workspace_bytes(NP), h->stream);
+    launch_hand_cc(avg, NP, H, W, lab, sums, cnt, pk, fo, ws, h->stream);
+    h->prof_end(pe);
+    hand_finish(h, N, peaks, found, flags & OPOSE_OUT_DEVICE);
+}
+
+int opose_batch_hand_post(opose_t* h, const float* maps, int N, int hl, int wl, const opose_params* pp, double* peaks,
+                          int32_t* found, int flags) {
+    if (!h || !maps || !peaks || !found || N <= 0 || hl <= 0 || wl <= 0) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const opose_params p = fill_params(pp, OPOSE_NET_HAND);
+        const size_t n_in = (size_t)N * 22 * hl * wl;
+        const float* md = maps;
+        if (!(flags & OPOSE_IN_DEVICE)) {
+            float* buf = h->maps_in.ensure<float>(n_in, h->stream);
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, maps, n_in * 4, hipMemcpyHostToDevice, h->stream));
+            md = buf;
+        }
+        batch_hand_post_common(h, N, 8 * hl, 8 * wl, md, 22, p, peaks, found, flags);
+    });
+    return OPOSE_OK;
+}
+
+int opose_batch_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride,
+                           int64_t frame_stride, const opose_params* pp, double* peaks, int32_t* found, int flags) {
+    if (!h || !bgr || !peaks || !found || N <= 0 || H <= 0 || W <= 0 || H % 8 || W % 8) return OPOSE_E_ARG;
+    if (row_stride < (int64_t)W * 3 || frame_stride < row_stride * H) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const opose_params p = fill_params(pp, OPOSE_NET_HAND);
+        const uint8_t* fd = bgr;
+        if (!(flags & OPOSE_IN_DEVICE)) {
+            uint8_t* buf = h->frames.ensure<uint8_t>((size_t)frame_stride * N, h->stream);
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, (size_t)frame_stride * N, hipMemcpyHostToDevice, h->stream));
+            fd = buf;
+        }
+        // ToTensor - 0.5 at scale 1 (torch bicubic at scale 1 is the identity)
+        float* x = h->x.ensure<float>((size_t)N * 3 * H * W, h->stream);
+        ProfEntry pe;
+        h->prof_begin(pe, "preprocess", 0, (double)N * 15.0 * H * W);
+        launch_preprocess_torch(fd, frame_stride, row_stride, N, H, W, H, W, 1.f, 1.f, H, W, x, h->stream);
+        h->prof_end(pe);
+        float* Sb = hand_net(h, x, N, H, W);
+        batch_hand_post_common(h, N, H, W, Sb, 150, p, peaks, found, flags);
+        hand_finish(h, N, peaks, found, flags & OPOSE_OUT_DEVICE);
+    });
+    return OPOSE_OK;
+}
+
 int opose_hand_infer_crops(opose_t* h, const uint8_t* const* crops, const int* sizes, const int64_t* row_strides,
                            int n, const opose_params* pp, double* peaks, int32_t* found, int flags) {
     if (!h || !crops || !sizes || !row_strides || !peaks || !found || n <= 0) return OPOSE_E_ARG;

@@ -54,6 +54,9 @@ void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double th
 // (srcmx/utilmx.py:230-243) on heat [NP][H][W] float; scores = blurred values
 void launch_blur5_nms(const float* heat, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
                       double* list_score, hipStream_t st);
+// Batch_hand fast mode: blurred (5x5, float64 out) + union-find seeds of blurred > thre
+void launch_blur5_seed(const float* heat, int NP, int H, int W, double thre, double* blurred, int* lab, int* cnt,
+                       hipStream_t st);
 void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st);
 void launch_peaks_finalize(const int* cnt, const int* list, const double* list_score, int N, int H, int W,
                            const RecordLayout& L, uint8_t* records, int* peak_pos, int* part_cnt, hipStream_t st);

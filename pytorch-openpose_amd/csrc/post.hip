@@ -237,6 +237,55 @@ __global__ __launch_bounds__(256) void blur5_nms(const float* __restrict__ heat,
     }
 }
 
+// Batch_hand fast mode (srcmx/Batch_model.py:327-354): blurred = 5x5 Gaussian of the x8 map
+// (float32); binary = blurred > thre seeds the union-find labelling (run starts, as
+// gauss_threshold); the blurred map (as float64) is what components are summed and searched
+// on.  64 x 16 tiles: one wave = one 64-pixel row segment.
+constexpr int SW = 64, SH = 16;
+__global__ __launch_bounds__(256) void blur5_seed(const float* __restrict__ heat, int H, int W, double thre,
+                                                  double* __restrict__ blurred, int* __restrict__ lab,
+                                                  int* __restrict__ cnt) {
+    __shared__ float s_in[SH + 4][SW + 4];
+    __shared__ int s_n;
+    const int ntx = (W + SW - 1) / SW, nty = (H + SH - 1) / SH;
+    const int total = gridDim.x, b = blockIdx.x;
+    const int q = total >> 3, rr = total & 7, xcd = b & 7;
+    const int id = xcd * q + min(xcd, rr) + (b >> 3);
+    const int tx = id % ntx, rest = id / ntx;
+    const int ty = rest % nty, np = rest / nty;
+    const int x0 = tx * SW, y0 = ty * SH;
+    const float* m = heat + (size_t)np * H * W;
+    if (threadIdx.x == 0) s_n = 0;
+    for (int e = threadIdx.x; e < (SH + 4) * (SW + 4); e += 256) {
+        const int r = e / (SW + 4), c = e - r * (SW + 4);
+        s_in[r][c] = m[(size_t)reflect101(y0 - 2 + r, H) * W + reflect101(x0 - 2 + c, W)];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    int mine = 0;
+    for (int e = threadIdx.x; e < SW * SH; e += 256) {
+        const int r = e / SW, c = e - r * SW;
+        const int y = y0 + r, x = x0 + c;
+        const bool in = y < H && x < W;
+        float acc = 0.f;
+#pragma unroll
+        for (int dy = 0; dy < 5; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 5; ++dx) acc = acc + s_in[r + dy][c + dx] * kBlur5[dy][dx];
+        const bool on = in && acc > (float)thre;
+        const unsigned long long unset = ~__ballot(on) & ((1ull << lane) - 1);
+        const int start = unset ? 64 - __clzll((long long)unset) : 0;
+        if (!in) continue;
+        const size_t i = (size_t)y * W + x;
+        blurred[(size_t)np * H * W + i] = (double)acc;
+        lab[(size_t)np * H * W + i] = on ? (int)i - (lane - start) : -1;
+        mine += on;
+    }
+    if (mine) atomicAdd(&s_n, mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_n) atomicAdd(cnt + np, s_n);
+}
+
 // One workgroup per frame: order each part's peaks row-major (np.nonzero), assign the
 // global running ids, write candidate rows (x, y, score, id) into the record.
 __global__ __launch_bounds__(256) void peaks_finalize(const int* __restrict__ cnt, const int* __restrict__ list,
@@ -543,6 +592,12 @@ void launch_blur5_nms(const float* heat, int NP, int H, int W, double thre, int 
                       double* list_score, hipStream_t st) {
     dim3 grid(((W + BT - 1) / BT) * ((H + BT - 1) / BT) * NP);
     hipLaunchKernelGGL(blur5_nms, grid, dim3(256), 0, st, heat, H, W, thre, cap, cnt, list, list_score);
+}
+
+void launch_blur5_seed(const float* heat, int NP, int H, int W, double thre, double* blurred, int* lab, int* cnt,
+                       hipStream_t st) {
+    dim3 grid(((W + SW - 1) / SW) * ((H + SH - 1) / SH) * NP);
+    hipLaunchKernelGGL(blur5_seed, grid, dim3(256), 0, st, heat, H, W, thre, blurred, lab, cnt);
 }
 
 void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st) {

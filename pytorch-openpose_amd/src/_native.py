@@ -52,6 +52,8 @@ def _load():
         "opose_hand_infer_crops": (I, [P, C.POINTER(P), P, P, I, C.POINTER(Params), P, P, I]),
         "opose_batch_body_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, I]),
         "opose_batch_body_post": (I, [P, P, I, I, I, I, I, I, I, C.POINTER(Params), P, I]),
+        "opose_batch_hand_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, P, I]),
+        "opose_batch_hand_post": (I, [P, P, I, I, I, C.POINTER(Params), P, P, I]),
         "opose_profile_enable": (I, [P, I]),
         "opose_profile_reset": (I, [P]),
         "opose_profile_read": (I, [P, C.c_char_p, S]),
@@ -73,7 +75,7 @@ lib = _load()
 EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last_error", "opose_set_stream",
             "opose_get_stream", "opose_synchronize", "opose_set_capacity", "opose_body_record_bytes",
             "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_body_infer",
-            "opose_body_post", "opose_batch_body_infer", "opose_batch_body_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
+            "opose_body_post", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
             "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_conv_time", "opose_debug_preprocess",
             "opose_debug_heat"]
 

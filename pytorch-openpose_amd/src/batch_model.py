@@ -96,3 +96,47 @@ class Batch_body(Body):
             self.handle.h, frames_dev.data_ptr(), N, H, W, frames_dev.stride(1), frames_dev.stride(0), self.params,
             records_dev.data_ptr(), _native.IN_DEVICE | _native.OUT_DEVICE))
         return records_dev
+
+
+class Batch_hand(object):
+    """srcmx/Batch_model.py:310-354: crops already resized to boxsize (the data loader's
+    HandImageDataset does that with cv2) -> np.array [B, 21, 3] of (x, y, score) in crop
+    pixels, float64 (int64 when nothing is found anywhere, as np.array of [0, 0, 0] rows)."""
+
+    def __init__(self, model_path, device: int = 0, thre=0.035):
+        from .hand import _load_state
+        from .model import handpose_model
+        from . import util
+        self.model = handpose_model(device)
+        self.model.load_state_dict(util.transfer(self.model, _load_state(model_path)))
+        self.model.eval()
+        self.handle = self.model.handle
+        self.params = _native.default_params(_native.NET_HAND, scale_search=(1.0,), thre_hand=float(thre))
+
+    def __call__(self, batch_imgs):
+        crops = np.ascontiguousarray(_as_uint8_frames(batch_imgs))
+        N, H, W, _ = crops.shape
+        peaks = np.empty((N, 21, 3), np.float64)
+        found = np.empty((N, 21), np.int32)
+        self.handle.check(_native.lib.opose_batch_hand_infer(self.handle.h, crops.ctypes.data, N, H, W,
+                                                             crops.strides[1], crops.strides[1] * H, self.params,
+                                                             peaks.ctypes.data, found.ctypes.data, 0))
+        return self._as_reference(peaks, found)
+
+    def post(self, heat):
+        """Post-network part only (srcmx/Batch_model.py:334-354): heat float32 [B, 22, hl, wl]."""
+        heat = np.ascontiguousarray(heat, dtype=np.float32)
+        N, c, hl, wl = heat.shape
+        assert c == 22
+        peaks = np.empty((N, 21, 3), np.float64)
+        found = np.empty((N, 21), np.int32)
+        self.handle.check(_native.lib.opose_batch_hand_post(self.handle.h, heat.ctypes.data, N, hl, wl, self.params,
+                                                            peaks.ctypes.data, found.ctypes.data, 0))
+        return self._as_reference(peaks, found)
+
+    @staticmethod
+    def _as_reference(peaks, found):
+        if not found.any():
+            return np.zeros(peaks.shape, dtype=np.int64)
+        peaks[~found.astype(bool)] = 0.0
+        return peaks

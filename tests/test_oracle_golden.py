@@ -141,3 +141,16 @@ def test_batch_oracle_e2e_matches_reference():
         assert np.array_equal(c[:, [0, 1, 3]], ref_c[:, [0, 1, 3]])
         np.testing.assert_allclose(c[:, 2], ref_c[:, 2], rtol=1e-5, atol=1e-6)
         assert np.array_equal(s[:, :18], ref_s[:, :18])
+
+
+def test_batch_hand_oracle_matches_reference():
+    import torch
+    from oracle import batch_post
+    d = np.load(os.path.join(GOLDEN, "batch_hand_planted_b4.npz"))
+    got = batch_post.hand_post(torch.from_numpy(d["heat"]))
+    assert got.dtype == d["peaks"].dtype and np.array_equal(got, d["peaks"])
+    d = np.load(os.path.join(GOLDEN, "batch_hand_e2e_b2_64.npz"))
+    sd = network.seeded_state_dict("hand", 0)
+    got = batch_post.batch_hand_infer(d["crops"], lambda x: network.hand_forward(torch.from_numpy(x), sd).numpy())
+    assert np.array_equal(got[:, :, :2], d["peaks"][:, :, :2])
+    np.testing.assert_allclose(got[:, :, 2], d["peaks"][:, :, 2], rtol=1e-5)
