@@ -116,6 +116,23 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W,
 int opose_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int pad_down,
                     int pad_right, int H, int W, const opose_params* p, void* records, int flags);
 
+/* ---- scale-sharded single-frame latency (one scale of src/body.py:34-50 per rank) ------- */
+/* Geometry of scale s of p->scales for an H x W frame (src/body.py:35-41): out4 = {hl, wl,
+ * pad_down, pad_right} = network output size and util.padRightDownCorner's pads. */
+int opose_body_scale_geom(int H, int W, const opose_params* p, int s, int* out4);
+
+/* Network maps of scale s only (src/body.py:36-50 for one m): maps [N,57,hl,wl] fp32
+ * (channels 0..37 PAF, 38..56 heat), host memory unless OPOSE_OUT_DEVICE. */
+int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride,
+                          int64_t frame_stride, const opose_params* p, int s, float* maps, int flags);
+
+/* Multi-scale post-network body path (src/body.py:51-203): maps[s] = [N,57,hl[s],wl[s]] of
+ * every scale (any rank's output of opose_body_scale_maps, gathered); the per-scale x8 /
+ * crop / resize, the float64 scale average and everything after it, as opose_body_infer. */
+int opose_body_post_scales(opose_t* h, const float* const* maps, const int* hl, const int* wl,
+                           const int* pad_down, const int* pad_right, int n_scales, int N, int H,
+                           int W, const opose_params* p, void* records, int flags);
+
 /* Batched "fast mode" of the reference (srcmx/Batch_model.py:137-204 Batch_body.__call__):
  * torch-bicubic pre/post-processing (inputs as transforms.ToTensor would give: uint8 / 255),
  * single scale p->scales[0] (Batch_body: 0.5), 5x5 Gaussian + peak scores from the blurred

@@ -1027,6 +1027,96 @@ int opose_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int pa
     });
 }
 
+// ---- scale-sharded single-frame latency ---------------------------------
+int opose_body_scale_geom(int H, int W, const opose_params* pp, int s, int* out4) {
+    if (!out4 || H <= 0 || W <= 0) return OPOSE_E_ARG;
+    try {
+        const opose_params p = fill_params(pp, OPOSE_NET_BODY);
+        if (s < 0 || s >= p.n_scales) return OPOSE_E_ARG;
+        const ScaleGeom g = geom(p.scales[s], p, H, W);
+        out4[0] = g.hl;
+        out4[1] = g.wl;
+        out4[2] = g.Hp - g.Hs;
+        out4[3] = g.Wp - g.Ws;
+        return OPOSE_OK;
+    } catch (const std::exception&) {
+        return OPOSE_E_SHAPE;
+    }
+}
+
+int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride,
+                          int64_t frame_stride, const opose_params* pp, int s, float* maps, int flags) {
+    if (!h || !bgr || !maps || N <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
+    if (row_stride < (int64_t)W * 3 || frame_stride < row_stride * H) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const opose_params p = fill_params(pp, OPOSE_NET_BODY);
+        if (s < 0 || s >= p.n_scales) return OPOSE_E_ARG;
+        const uint8_t* fd = bgr;
+        if (!(flags & OPOSE_IN_DEVICE)) {
+            uint8_t* buf = h->frames.ensure<uint8_t>((size_t)frame_stride * N, h->stream);
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, (size_t)frame_stride * N, hipMemcpyHostToDevice, h->stream));
+            fd = buf;
+        }
+        const ScaleGeom g = geom(p.scales[s], p, H, W);
+        float* x = h->x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
+        launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp, g.Wp,
+                          (float)p.pad_value / 256.f - 0.5f, x, h->stream);
+        const float* S = body_net(h, x, N, g.Hp, g.Wp);
+        // channels 0..56 of the stage-6 concat buffer [N][185][hl*wl] -> [N][57][hl*wl]
+        const size_t plane = (size_t)g.hl * g.wl * 4;
+        OPOSE_HIP_CHECK(hipMemcpy2DAsync(maps, 57 * plane, S, 185 * plane, 57 * plane, N,
+                                         (flags & OPOSE_OUT_DEVICE) ? hipMemcpyDeviceToDevice
+                                                                    : hipMemcpyDeviceToHost,
+                                         h->stream));
+        if (!(flags & OPOSE_OUT_DEVICE)) OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+        return OPOSE_OK;
+    });
+}
+
+int opose_body_post_scales(opose_t* h, const float* const* maps, const int* hl, const int* wl, const int* pad_down,
+                           const int* pad_right, int n_scales, int N, int H, int W, const opose_params* pp,
+                           void* records, int flags) {
+    if (!h || !maps || !hl || !wl || !pad_down || !pad_right || !records || N <= 0 || H <= 0 || W <= 0 ||
+        n_scales < 1 || n_scales > OPOSE_MAX_SCALES)
+        return OPOSE_E_ARG;
+    for (int s = 0; s < n_scales; ++s)
+        if (!maps[s] || hl[s] <= 0 || wl[s] <= 0 || pad_down[s] < 0 || pad_right[s] < 0 ||
+            pad_down[s] >= 8 * hl[s] || pad_right[s] >= 8 * wl[s])
+            return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        opose_params p = fill_params(pp, OPOSE_NET_BODY);
+        const RecordLayout L = make_record_layout(h->ppp, h->maxp);
+        std::vector<ScaleGeom> gs;
+        for (int s = 0; s < n_scales; ++s) {
+            ScaleGeom g;
+            g.mult = 0;
+            g.hl = hl[s];
+            g.wl = wl[s];
+            g.Hp = 8 * hl[s];
+            g.Wp = 8 * wl[s];
+            g.Hs = g.Hp - pad_down[s];
+            g.Ws = g.Wp - pad_right[s];
+            g.up_sy = 1.0 / ((double)H / g.Hs);
+            g.up_sx = 1.0 / ((double)W / g.Ws);
+            const float* md = maps[s];
+            if (!(flags & OPOSE_IN_DEVICE)) {
+                const size_t n_in = (size_t)N * 57 * g.hl * g.wl;
+                float* buf = h->maps_in.ensure<float>(n_in, h->stream);
+                OPOSE_HIP_CHECK(hipMemcpyAsync(buf, maps[s], n_in * 4, hipMemcpyHostToDevice, h->stream));
+                md = buf;
+            }
+            upsample_to_mid(h, s, md, 57, N, g, 56);
+            gs.push_back(g);
+        }
+        uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)
+                                                  : h->records.ensure<uint8_t>(L.bytes * N, h->stream);
+        body_post_common(h, N, H, W, gs, p, rec);
+        return finish_records(h, N, records, rec, flags);
+    });
+}
+
 int opose_batch_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride,
                            int64_t frame_stride, const opose_params* pp, void* records, int flags) {
     if (!h || !bgr || !records || N <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;

@@ -47,6 +47,9 @@ def _load():
         "opose_hand_forward": (I, [P, P, I, I, I, P, I]),
         "opose_body_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, I]),
         "opose_body_post": (I, [P, P, I, I, I, I, I, I, I, C.POINTER(Params), P, I]),
+        "opose_body_scale_geom": (I, [I, I, C.POINTER(Params), I, P]),
+        "opose_body_scale_maps": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), I, P, I]),
+        "opose_body_post_scales": (I, [P, C.POINTER(P), P, P, P, P, I, I, I, I, C.POINTER(Params), P, I]),
         "opose_hand_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, P, I]),
         "opose_hand_post": (I, [P, C.POINTER(P), P, P, P, P, I, I, I, I, C.POINTER(Params), P, P, I]),
         "opose_hand_infer_crops": (I, [P, C.POINTER(P), P, P, I, C.POINTER(Params), P, P, I]),
@@ -75,7 +78,8 @@ lib = _load()
 EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last_error", "opose_set_stream",
             "opose_get_stream", "opose_synchronize", "opose_set_capacity", "opose_body_record_bytes",
             "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_body_infer",
-            "opose_body_post", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
+            "opose_body_post", "opose_body_scale_geom", "opose_body_scale_maps",
+            "opose_body_post_scales", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
             "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_conv_time", "opose_debug_preprocess",
             "opose_debug_heat"]
 

@@ -19,6 +19,8 @@ the device (multi-GPU gather, benchmark).
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
 from . import _native, util
@@ -30,6 +32,9 @@ def _load_state(model_path):
         return model_path
     import torch
     return torch.load(model_path, map_location="cpu", weights_only=True)
+
+
+ctypes_int4 = ctypes.c_int * 4
 
 
 class Body(object):
@@ -84,6 +89,73 @@ class Body(object):
             rec = np.empty((N, self.handle.record_bytes()), np.uint8)
             rc = _native.lib.opose_body_post(self.handle.h, maps.ctypes.data, N, hl, wl, int(pad[2]), int(pad[3]),
                                              int(H), int(W), self.params, rec.ctypes.data, 0)
+            if rc == _native.OPOSE_E_CAPACITY and self._grow():
+                continue
+            if rc not in (_native.OPOSE_OK, _native.OPOSE_E_CAPACITY, _native.OPOSE_E_ASSEMBLY):
+                self.handle.check(rc)
+            return [self._decode(r) for r in rec]
+
+    # ------------------------------------------------------------------ per-scale split
+    def scale_geom(self, H, W):
+        """[(hl, wl, pad_down, pad_right)] per scale of scale_search for an H x W frame."""
+        out = []
+        for s in range(self.params.n_scales):
+            g = (ctypes_int4)()
+            self.handle.check(_native.lib.opose_body_scale_geom(int(H), int(W), self.params, s, g))
+            out.append(tuple(int(v) for v in g))
+        return out
+
+    def scale_maps(self, frames, s, out=None):
+        """Network maps of scale index `s` only: [N, 57, hl, wl] float32 (PAF 38 | heat 19).
+
+        frames: uint8 [N,H,W,3] numpy (-> numpy) or a torch cuda tensor (-> torch cuda tensor,
+        written into `out` when given; the handle's stream is synchronised before returning)."""
+        if hasattr(frames, "data_ptr"):
+            import torch
+            if frames.dim() == 3:
+                frames = frames[None]
+            N, H, W, _ = frames.shape
+            if frames.stride(2) != 3 or frames.stride(3) != 1 or (N > 1 and frames.stride(0) < frames.stride(1) * H):
+                raise ValueError("expected uint8 frames [N, H, W, 3] with packed pixels")
+            hl, wl, _, _ = self.scale_geom(H, W)[s]
+            if out is None:
+                out = torch.empty((N, 57, hl, wl), dtype=torch.float32, device=frames.device)
+            assert out.is_contiguous() and tuple(out.shape) == (N, 57, hl, wl)
+            self.handle.check(_native.lib.opose_body_scale_maps(
+                self.handle.h, frames.data_ptr(), N, H, W, frames.stride(1), max(frames.stride(0), frames.stride(1) * H),
+                self.params, s, out.data_ptr(), _native.IN_DEVICE | _native.OUT_DEVICE))
+            self.handle.check(_native.lib.opose_synchronize(self.handle.h))
+            return out
+        frames = np.ascontiguousarray(frames if np.ndim(frames) == 4 else np.asarray(frames)[None])
+        N, H, W, _ = frames.shape
+        hl, wl, _, _ = self.scale_geom(H, W)[s]
+        maps = np.empty((N, 57, hl, wl), np.float32)
+        self.handle.check(_native.lib.opose_body_scale_maps(
+            self.handle.h, frames.ctypes.data, N, H, W, frames.strides[1], frames.strides[1] * H, self.params, s,
+            maps.ctypes.data, 0))
+        return maps
+
+    def post_scales(self, maps, H, W):
+        """Multi-scale post-network path (src/body.py:51-212): maps[s] = [N,57,hl,wl] for every
+        scale of scale_search (numpy, or torch cuda tensors) -> list of (candidate, subset)."""
+        geoms = self.scale_geom(H, W)
+        if len(maps) != len(geoms):
+            raise ValueError("expected %d scale maps, got %d" % (len(geoms), len(maps)))
+        dev = hasattr(maps[0], "data_ptr")
+        if not dev:
+            maps = [np.ascontiguousarray(m, dtype=np.float32) for m in maps]
+        for m, (hl, wl, _, _) in zip(maps, geoms):
+            if tuple(m.shape[1:]) != (57, hl, wl):
+                raise ValueError("scale maps of shape %s, expected (N, 57, %d, %d)" % (tuple(m.shape), hl, wl))
+        N = maps[0].shape[0]
+        ns = len(maps)
+        ptrs = (ctypes.c_void_p * ns)(*[m.data_ptr() if dev else m.ctypes.data for m in maps])
+        arr = [(ctypes.c_int * ns)(*[g[i] for g in geoms]) for i in range(4)]
+        while True:
+            rec = np.empty((N, self.handle.record_bytes()), np.uint8)
+            rc = _native.lib.opose_body_post_scales(self.handle.h, ptrs, arr[0], arr[1], arr[2], arr[3], ns, N,
+                                                    int(H), int(W), self.params, rec.ctypes.data,
+                                                    _native.IN_DEVICE if dev else 0)
             if rc == _native.OPOSE_E_CAPACITY and self._grow():
                 continue
             if rc not in (_native.OPOSE_OK, _native.OPOSE_E_CAPACITY, _native.OPOSE_E_ASSEMBLY):

@@ -117,6 +117,30 @@ def main():
     st = rec5.view(torch.int32)[:, 0].cpu().numpy()
     out["C5_status_nonzero"] = int((st != 0).sum())
     out["C5_mean_peaks_people"] = rec5.view(torch.int32)[:, 1:3].float().mean(0).cpu().tolist()
+
+    # C5 single-frame latency: all four scales on one GPU vs the scale-sharded split
+    # (src.dist.body_scale_sharded): per-scale network time and the multi-scale post on the
+    # gathered low-res maps, measured here; the sharded latency is max over ranks of its scales'
+    # network time + the gather of <= 3.4 MB low-res maps per scale + the post on rank 0.
+    from src.dist import scale_plan
+    f1 = f5[:1].contiguous()
+    rec1 = rec5[:1]
+
+    def one5():
+        body5.infer_records(f1, rec1)
+        body5.handle.synchronize()
+    out["C5_single_frame_latency_ms"] = timed(one5, 10, warm=2)
+    geoms = body5.scale_geom(1080, 1920)
+    maps = [body5.scale_maps(f1, s) for s in range(len(geoms))]
+    net_ms = [timed(lambda s=s: body5.scale_maps(f1, s, out=maps[s]), 10, warm=1) for s in range(len(geoms))]
+    post_ms = timed(lambda: body5.post_scales(maps, 1080, 1920), 10, warm=1)
+    out["C5_scale_net_ms"] = net_ms
+    out["C5_scale_lowres_mb"] = [4 * 57 * g[0] * g[1] / 1e6 for g in geoms]
+    out["C5_post_scales_ms"] = post_ms
+    for world in (2, 4):
+        own = scale_plan([g[0] * g[1] for g in geoms], world)
+        load = [sum(t for t, r in zip(net_ms, own) if r == k) for k in range(world)]
+        out["C5_sharded_w%d_model_ms_excl_gather" % world] = max(load) + post_ms
     print(json.dumps(out))
 
 

@@ -76,3 +76,81 @@ def test_shard_bounds_cover_exactly():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+# ------------------------------------------------------------- single-frame scale sharding
+GEOMS = [(12, 20, 4, 0), (23, 40, 0, 0), (35, 60, 4, 4), (46, 80, 0, 0)]   # C5-like pyramid, scaled down
+
+
+class _FakeBody:
+    """Stands in for Body: per-scale maps are a function of the scale only, post returns them."""
+
+    def __init__(self):
+        self.computed = []
+
+    def scale_geom(self, H, W):
+        return GEOMS
+
+    def scale_maps(self, frame, s):
+        self.computed.append(s)
+        hl, wl = GEOMS[s][:2]
+        rng = np.random.default_rng(100 + s)
+        return rng.standard_normal((frame.shape[0], 57, hl, wl)).astype(np.float32)
+
+    def post_scales(self, maps, H, W):
+        return [np.asarray(m) for m in maps]
+
+
+def _scale_worker(rank, world, port, q):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from src.dist import body_scale_sharded, scale_plan
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        body = _FakeBody()
+        frame = np.zeros((90, 160, 3), np.uint8)
+        out = body_scale_sharded(body, frame, rank, world, dst=0)
+        owner = scale_plan([g[0] * g[1] for g in GEOMS], world)
+        ok = sorted(body.computed) == [s for s, r in enumerate(owner) if r == rank]
+        if rank == 0:
+            ok &= len(out) == len(GEOMS)
+            for s, m in enumerate(out):
+                ok &= np.array_equal(m, _FakeBody().scale_maps(frame[None], s))
+        else:
+            ok &= out is None
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_scale_sharded_gathers_lowres_maps(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29900 + world * 13 + os.getpid() % 200
+    procs = [ctx.Process(target=_scale_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}
+
+
+def test_scale_plan_balances_largest_first():
+    import sys
+    sys.path.insert(0, PKG)
+    from src.dist import scale_plan
+    costs = [0.25, 1.0, 2.25, 4.0]          # scale_search = [0.5, 1, 1.5, 2]: cost ~ scale^2
+    assert scale_plan(costs, 1) == [0, 0, 0, 0]
+    assert scale_plan(costs, 2) == [1, 1, 1, 0]           # 4.0 | 3.5
+    assert scale_plan(costs, 4) == [3, 2, 1, 0]
+    assert scale_plan(costs, 8) == [3, 2, 1, 0]
+    for w in (2, 3, 5):
+        own = scale_plan(costs, w)
+        load = [sum(c for c, r in zip(costs, own) if r == k) for k in range(w)]
+        assert max(load) == 4.0
