@@ -9,8 +9,11 @@ Frames shard across ranks (weak scaling: B frames per GPU).  Weights are seeded 
 (real .pth files are unavailable offline).
 
 Prints ONE JSON line on rank 0 (driver contract) including:
-* roofline: the 7x7-conv kernel class (68 % of network FLOPs), algorithmic FLOPs per launch
-  / mean launch time from HIP events recorded on the library's stream inside the timed region;
+* roofline: the 7x7-conv kernel class (68 % of network FLOPs), algorithmic (fp32) FLOPs per
+  launch / mean launch time from HIP events recorded on the library's stream inside the timed
+  region, against the ceiling of the kernel that ran: the split-bf16 conv (default; six bf16
+  MFMA piece products per fp32 multiply-add -> bf16 peak / 6) or the fp32 MFMA conv
+  (OPOSE_CONV=f32 -> fp32 MFMA peak);
 * cpu_baseline: the oracle (torch-CPU conv graph + NumPy/SciPy post-processing, proven
   identical to the reference on the golden fixtures) on a bounded sample of the same workload.
 """
@@ -33,6 +36,13 @@ for p in (PKG, REPO):
 
 H, W = 368, 656
 PEAK_FP32_TFLOPS = 157.3  # MI355X fp32 matrix peak (MI355X_MICROARCH.md: spec 157.3, 155 measured)
+PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA peak (no sparsity)
+# The network runs on the split-bf16 conv kernel (csrc/conv_x6.hip) unless OPOSE_CONV=f32: one
+# fp32-equivalent multiply-add = 6 bf16 MFMA piece products, so its ceiling in fp32-equivalent
+# (algorithmic) FLOP/s is the bf16 peak / 6.
+X6 = os.environ.get("OPOSE_CONV", "x6") != "f32"
+PEAK_CONV_TFLOPS = PEAK_BF16_TFLOPS / 6 if X6 else PEAK_FP32_TFLOPS
+CONV_KERNEL = "conv_x6" if X6 else "conv_igemm_f32"
 
 
 def parse():
@@ -56,11 +66,12 @@ def pmc_traffic():
         rec = json.load(open(path))
     except (OSError, ValueError):
         return None
-    # the 7x7 class runs one kernel instantiation (conv_igemm_f32<MT, PT, true, 7, 0>); take
-    # the 7x7 instantiation with the most dispatches
+    # the 7x7 class runs one kernel instantiation (conv_x6<MT, PT, false, 7> /
+    # conv_igemm_f32<MT, PT, true, 7, 0>); take the 7x7 instantiation with the most dispatches
     best = None
+    tag = ", false, 7>" if X6 else ", true, 7, 0>"
     for name, v in rec.items():
-        if "conv_igemm_f32<" in name and ", true, 7, 0>" in name and "hbm_bytes_per_launch" in v:
+        if CONV_KERNEL + "<" in name and tag in name and "hbm_bytes_per_launch" in v:
             if best is None or v.get("trace_calls", 0) > best.get("trace_calls", 0):
                 best = v
     return best["hbm_bytes_per_launch"] if best else None
@@ -81,8 +92,8 @@ def stage_roofline(prof):
             continue
         if k.startswith("conv"):
             a = v["flops"] / (v["ms"] * 1e-3) / 1e12
-            out[k] = {"bound": "mfma", "achieved": round(a, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                      "frac": round(a / PEAK_FP32_TFLOPS, 4)}
+            out[k] = {"bound": "mfma", "achieved": round(a, 2), "peak": round(PEAK_CONV_TFLOPS, 1),
+                      "unit": "TFLOP/s", "frac": round(a / PEAK_CONV_TFLOPS, 4)}
         elif k in LATENCY_STAGES or v.get("bytes", 0) <= 0:
             out[k] = {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None}
         else:
@@ -215,14 +226,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "conv_arithmetic": ("fp32-accurate split-bf16 MFMA: x = x0+x1+x2 (bf16, exact), 6 piece products, "
+                                "fp32 accumulate (tests/test_gpu_x6.py)") if X6 else "fp32 MFMA",
             "data": "synthetic (uniform uint8 frames, seeded He-normal weights; real weights unavailable offline)",
             "config": {"workload": f"C2/C4: Body() on 368x656 frames, {B} frames per GPU per step, "
                                    f"RCCL all_gather of per-frame keypoint records when n_gpus > 1",
                        "frame": [H, W], "frames_per_gpu_per_step": B, "scale_search": [0.5],
                        "net_input": [184, 328], "parallelism": f"frame-sharded dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "conv_igemm_f32 (7x7 CPM stages)",
-                         "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_TFLOPS,
+            "roofline": {"bound": "mfma", "kernel": CONV_KERNEL + " (7x7 CPM stages)",
+                         "achieved": achieved, "peak": PEAK_CONV_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_CONV_TFLOPS,
+                         "peak_basis": ("dense bf16 MFMA peak 2500 / 6 piece products per fp32-equivalent "
+                                        "multiply-add (algorithmic fp32 FLOPs)") if X6 else "fp32 MFMA peak",
                          "per_launch_flops": c7["flops"] / max(1, c7["count"]),
                          "mean_launch_ms": c7["ms"] / max(1, c7["count"]), "traffic": pmc_traffic(),
                          "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE)*1KiB, profiles/pmc_summary.json"},

@@ -198,6 +198,14 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
  * launches; ablate bit 1 skips the im2col gather, bit 2 the weight load (timing only) */
 int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, int ks, int ngroups,
                           int mt, int pt, int splits, int ablate, int reps, float* ms);
+/* The split-bf16 ("x6") conv kernel on one layer: x fp32 NCHW is split into three bf16 pieces,
+ * convolved with six bf16 MFMA piece products per fp32 product, written fp32 (out_x6 = 0) or
+ * split and rebuilt (out_x6 = 1). */
+int opose_debug_conv_x6(opose_t* h, const float* x, const float* w, const float* b, int N, int Cin, int H,
+                        int W, int Cout, int ks, int pad, int relu, int mt, int pt, int splits, int out_x6,
+                        float* out);
+int opose_debug_conv_x6_time(opose_t* h, int N, int Cin, int H, int W, int Cout, int ks, int ngroups,
+                             int mt, int pt, int splits, int reps, float* ms);
 /* src/body.py:38-41 for one frame and one scale: out [3,Hp,Wp]; HpWp receives (Hp, Wp)
  * (out may be NULL to query the size) */
 int opose_debug_preprocess(opose_t* h, const uint8_t* bgr, int H, int W, double scale, int pad_value,

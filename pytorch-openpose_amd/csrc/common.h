@@ -50,6 +50,35 @@ struct ConvArgs {
                         // workgroup of a split tile reduces it; nullptr: conv_sk_fixup launch
 };
 
+// ---------------------------------------------------------------- split-bf16 ("x6") convolution
+// Activation format X6: every fp32 value x is stored as three bfloat16 pieces x0 + x1 + x2 == x
+// (exact: round-to-nearest bf16 of x, of the remainder, of the remainder's remainder -> 24
+// significant bits = the whole fp32 significand).  Layout per piece plane: [N][Cg][H*W][8]
+// (8 channels of a pixel contiguous = one 16-byte unit); the three planes follow each other
+// at `ps` bytes.  Channel offsets / strides are in groups of 8 channels.
+struct X6Group {
+    const uint8_t* in;     // X6 buffer (plane 0, frame 0, group 0)
+    const uint8_t* wt;     // [nK][3 pieces][4 groups][Mpad] units of 8 bf16
+    const float* bias;     // [cout]
+    void* out;             // X6 buffer, or fp32 NCHW when out_f32
+    void* out2;            // optional duplicate destination, same format (nullptr = none)
+    uint32_t in_ps, out_ps, out2_ps;  // piece strides (bytes) of the X6 buffers
+    int in_cg, in_goff;    // groups per frame of the input buffer / first group read
+    int out_c, out_off;    // X6: groups per frame / first group; fp32: channels / first channel
+    int out2_c, out2_off;
+    int cout, relu, out_f32;
+};
+
+struct X6Args {
+    X6Group g[2];
+    int N, H, W, ks, pad;
+    int cin_g;      // channel groups of the conv's input (Cin padded to 8)
+    int small;      // 1: one group (Cin <= 8), chunks of 4 taps; 0: chunks of (4 groups, 1 tap)
+    int nK;         // chunks of 32 k
+    int Mpad, npix, ngroups, sk_grid;
+    float* partial; // stream-K partial slabs [2 * sk_grid][MT * PT]
+};
+
 // ---------------------------------------------------------------- body records
 struct RecordLayout {
     int peaks_per_part;  // capacity per part

@@ -1,0 +1,586 @@
+// conv_x6.hip — fp32-accurate implicit-GEMM convolution on the gfx950 bf16 matrix cores.
+//
+// Same GEMM view as conv.hip (out[m][p] = bias[m] + sum_k W[m][k] im2col[k][p], src/model.py
+// make_layers / forward), but every fp32 operand is carried as three bfloat16 pieces
+// (x = x0 + x1 + x2 exactly, see common.h X6) and each product is rebuilt from the six
+// piece products whose weight is >= 2^-16 of the leading one:
+//     a*b ~= a0 b0 + (a0 b1 + a1 b0) + (a0 b2 + a1 b1 + a2 b0)
+// The dropped terms (a1 b2 + a2 b1 + a2 b2) are below 2^-23 |a b|, the size of one fp32
+// rounding, and every piece product is exact in the fp32 accumulator: the sum carries fp32
+// rounding error like the v_mfma_f32_32x32x2_f32 kernel (tests/test_gpu_x6.py measures both
+// against a float64 reference).  v_mfma_f32_32x32x16_bf16 issues 16x the FLOPs per cycle of
+// the fp32 MFMA, so six of them are 2.7x the fp32 MFMA rate.
+//
+// * Operand units are 16 bytes = 8 consecutive k of one row (A) / pixel (B): exactly the
+//   per-lane fragment of the 32x32x16 MFMA (lane l: row l&31, k = 8 (l>>5) .. +7), so LDS
+//   tiles are [piece][group][row] unit arrays read with one ds_read_b128 per fragment.
+// * Both tiles are filled by LDS-DMA: weights (pre-split, [chunk][piece][group][Mpad] units)
+//   by global_load_lds_dwordx4, the im2col pixels of a (piece, channel group, tap) by
+//   buffer_load_dwordx4 ... lds with the zero padding from the buffer range check.
+// * K chunk = 32 k = 4 channel groups of one tap (or 4 taps of a single group when Cin <= 8),
+//   two LDS stages, one barrier per chunk; stream-K ranges, partial slabs and the k-ordered
+//   fixup exactly as conv.hip.
+// * The epilogue adds bias, applies ReLU and writes the output split again (X6) into a
+//   group slice of a wider buffer (the CPM concat), or fp32 NCHW for the network outputs.
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace opose {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+namespace {
+
+constexpr int x6_waves(int mt, int pt) { return mt * pt >= 32768 ? 8 : 4; }
+
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+    uint32_t u = __float_as_uint(x);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return u >> 16;
+}
+
+// x -> three bf16 pieces, x0 + x1 + x2 == x exactly (each remainder is exact by Sterbenz)
+__device__ __forceinline__ void split3(float x, uint32_t& h0, uint32_t& h1, uint32_t& h2) {
+    h0 = bf16_rne(x);
+    const float r = x - __uint_as_float(h0 << 16);
+    h1 = bf16_rne(r);
+    const float r2 = r - __uint_as_float(h1 << 16);
+    h2 = bf16_rne(r2);
+}
+
+__device__ __forceinline__ float join3(uint32_t h0, uint32_t h1, uint32_t h2) {
+    return (__uint_as_float(h0 << 16) + __uint_as_float(h1 << 16)) + __uint_as_float(h2 << 16);
+}
+
+// write 4 consecutive channels (4hk .. 4hk+3 of a group) of one pixel, split, into the 3 planes
+__device__ __forceinline__ void store4_x6(uint8_t* unit, uint32_t ps, const float (&v)[4]) {
+    uint32_t h[3][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) split3(v[t], h[0][t], h[1][t], h[2][t]);
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+        uint2 w;
+        w.x = h[pc][0] | (h[pc][1] << 16);
+        w.y = h[pc][2] | (h[pc][3] << 16);
+        *reinterpret_cast<uint2*>(unit + (size_t)pc * ps) = w;
+    }
+}
+
+}  // namespace
+
+template <int MT, int PT, bool SMALL, int KS>
+__global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
+    const int ks = KS ? KS : a.ks;
+    const int taps = ks * ks;
+    constexpr int NW = x6_waves(MT, PT), NWM = NW == 8 ? MT / 64 : 2, NWP = NW / NWM;
+    constexpr int WM = MT / NWM, WP = PT / NWP;
+    constexpr int TM = WM / 32, TN = WP / 32;
+    constexpr int PJ = PT / 64;                  // 64-pixel runs per tile
+    constexpr int A_U = 12 * MT, B_U = 12 * PT;  // 16-byte units per stage
+    constexpr int A_PW = A_U / 64 / NW;          // A DMA instructions per wave per chunk
+    constexpr int WPJ = NW / PJ;                 // waves sharing one pixel run
+    constexpr int B_PW = 12 / WPJ;               // B DMA instructions per wave per chunk
+    static_assert(NW % PJ == 0 && 12 % WPJ == 0 && A_U % (64 * NW) == 0, "x6 tile");
+
+    __shared__ __attribute__((aligned(16))) uint4 lds[2 * (A_U + B_U)];
+    __shared__ float s_bias[MT];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l31 = lane & 31, hk = lane >> 5;
+    const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
+    const int nK = a.nK;
+    const int HW = a.H * a.W;
+    const int wm0 = (wave % NWM) * WM;
+    const int wp0 = (wave / NWM) * WP;
+    const int jw = wave % PJ;    // this wave's pixel run for the im2col DMA
+    const int pg0 = wave / PJ;   // its first (piece, group) row; then every WPJ-th
+
+    const int Gw = gridDim.x;
+    const int b = blockIdx.x;
+    const int q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
+    const int id = xcd * q + min(xcd, rr) + (b >> 3);
+    const long long I = (long long)nM * nP * a.ngroups * nK;
+    const long long lo = (long long)id * I / Gw, hi = (long long)(id + 1) * I / Gw;
+
+    for (long long itp = hi; itp > lo;) {
+        const int tile = (int)((itp - 1) / nK);
+        const int c_end = (int)(itp - (long long)tile * nK);
+        const int c_begin = (int)max<long long>(0, lo - (long long)tile * nK);
+        itp = (long long)tile * nK + c_begin;
+        const int first = itp == lo;
+        const int mt = tile % nM;
+        const int rest = tile / nM;
+        const int pt = rest % nP;
+        const int g = rest / nP;
+        const X6Group G = g == 0 ? a.g[0] : a.g[1];
+        const int p0 = pt * PT;
+        const int m0 = mt * MT;
+
+        __syncthreads();
+        if (tid < MT) s_bias[tid] = (m0 + tid < G.cout) ? G.bias[m0 + tid] : 0.f;
+
+        // the lane's im2col pixel (run jw): byte offset of its unit in group 0, plane 0
+        const uint8_t* in_base = G.in + (size_t)G.in_goff * HW * 16;
+        int py, px;
+        uint32_t pbase;
+        {
+            const int p = p0 + jw * 64 + lane;
+            const bool v = p < a.npix;
+            const int pc = v ? p : 0;
+            const int n = pc / HW;
+            const int r = pc - n * HW;
+            py = v ? r / a.W : -100000;
+            px = r - (r / a.W) * a.W;
+            pbase = (uint32_t)(n * G.in_cg * HW + r) * 16u;
+        }
+
+        floatx16 acc[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+        auto tap_off = [&](int tap) __attribute__((always_inline)) -> uint32_t {
+            const int ky = tap / ks;
+            const int dy = ky - a.pad, dx = tap - ky * ks - a.pad;
+            const int iy = py + dy, ix = px + dx;
+            const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+            return ok ? pbase + (uint32_t)((dy * a.W + dx) * 16) : 0x80000000u;  // >= num_records -> 0
+        };
+        // im2col DMA of chunk c into stage buf: (piece, group) rows pg0, pg0 + WPJ, ...
+        auto dma_b = [&](int c, int buf) __attribute__((always_inline)) {
+            uint4* Bs = lds + buf * (A_U + B_U) + A_U;
+            uint32_t voff = 0;
+            int cb = 0;
+            if constexpr (!SMALL) {
+                cb = c / taps;
+                voff = tap_off(c - cb * taps);
+            }
+#pragma unroll
+            for (int u = 0; u < B_PW; ++u) {
+                const int pg = pg0 + u * WPJ;
+                const int pc = pg >> 2, gi = pg & 3;
+                int grp;
+                uint32_t off;
+                if constexpr (SMALL) {
+                    grp = 0;
+                    off = tap_off(min(c * 4 + gi, taps - 1));  // padded taps: weights are 0
+                } else {
+                    grp = min(cb * 4 + gi, a.cin_g - 1);  // padded groups: any valid data (weights 0)
+                    off = voff;
+                }
+                const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                    (void*)(in_base + (size_t)pc * G.in_ps + (size_t)grp * HW * 16), (short)0, (int)0x80000000u,
+                    0x00020000);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + pg * PT + jw * 64), 16, off, 0, 0, 0);
+            }
+        };
+        auto dma_a = [&](int c, int buf) __attribute__((always_inline)) {
+            uint4* As = lds + buf * (A_U + B_U);
+#pragma unroll
+            for (int u = 0; u < A_PW; ++u) {
+                const int unit0 = (wave * A_PW + u) * 64;
+                const int pg = unit0 / MT, m = unit0 - pg * MT;
+                const uint8_t* src = G.wt + (((size_t)c * 12 + pg) * a.Mpad + m0 + m + lane) * 16;
+                __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + unit0), 16, 0, 0);
+            }
+        };
+
+        dma_a(c_begin, 0);
+        dma_b(c_begin, 0);
+        __syncthreads();
+        for (int c = c_begin; c < c_end; ++c) {
+            const int buf = (c - c_begin) & 1;
+            const int cn = min(c + 1, c_end - 1);  // the last chunk re-loads itself into the free stage
+            const uint32_t a_lds =
+                (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + hk * MT + wm0 + l31);
+            const uint32_t b_lds =
+                (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + A_U + hk * PT + wp0 + l31);
+            i32x4 fa[2][3][TM], fb[2][3][TN];
+            auto read_step = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+                        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                                     : "=v"(fa[s][pc][i])
+                                     : "v"(a_lds), "i"(((pc * 4 + 2 * s) * MT + 32 * i) * 16));
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                                     : "=v"(fb[s][pc][j])
+                                     : "v"(b_lds), "i"(((pc * 4 + 2 * s) * PT + 32 * j) * 16));
+                }
+            };
+            auto mfma_step = [&](int s) __attribute__((always_inline)) {
+                // small terms first: (2,0) (1,1) (0,2) (1,0) (0,1) (0,0)
+                constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
+                constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+                for (int t = 0; t < 6; ++t)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                __builtin_bit_cast(bf16x8, fa[s][PA[t]][i]), __builtin_bit_cast(bf16x8, fb[s][PB[t]][j]),
+                                acc[i][j], 0, 0, 0);
+            };
+            read_step(0);
+            dma_a(cn, buf ^ 1);
+            dma_b(cn, buf ^ 1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[0][pc][i]));
+#pragma unroll
+                for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(fb[0][pc][j]));
+            }
+            read_step(1);
+            mfma_step(0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[1][pc][i]));
+#pragma unroll
+                for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(fb[1][pc][j]));
+            }
+            mfma_step(1);
+            __syncthreads();  // next stage landed everywhere; this stage free
+        }
+
+        // ---- epilogue
+        const bool whole = c_begin == 0 && c_end == nK;
+        float* slab = a.partial + (size_t)(2 * id + (first ? 0 : 1)) * (MT * PT);
+        const int cout8 = (G.cout + 7) & ~7;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int pl = wp0 + j * 32 + l31;
+            const int p = p0 + pl;
+            if (!whole) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int ml = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
+                        asm volatile("global_store_dword %0, %1, off sc1" ::"v"(slab + ml * PT + pl),
+                                     "v"(acc[i][j][r])
+                                     : "memory");
+                    }
+                continue;
+            }
+            if (p >= a.npix) continue;
+            const int n = p / HW;
+            const int rem = p - n * HW;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd) {
+                    const int mg = m0 + wm0 + i * 32 + 8 * qd;  // first channel of the 8-group
+                    float v[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        v[t] = acc[i][j][4 * qd + t] + s_bias[mg - m0 + 4 * hk + t];
+                        if (G.relu) v[t] = fmaxf(v[t], 0.f);
+                    }
+                    if (G.out_f32) {
+                        float* ob = static_cast<float*>(G.out) + ((size_t)n * G.out_c + G.out_off) * HW + rem;
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int m = mg + 4 * hk + t;
+                            if (m < G.cout) ob[(size_t)m * HW] = v[t];
+                        }
+                    } else if (mg < cout8) {
+                        const int grp = mg >> 3;
+                        store4_x6(static_cast<uint8_t*>(G.out) +
+                                      ((size_t)(n * G.out_c + G.out_off + grp) * HW + rem) * 16 + hk * 8,
+                                  G.out_ps, v);
+                        if (G.out2)
+                            store4_x6(static_cast<uint8_t*>(G.out2) +
+                                          ((size_t)(n * G.out2_c + G.out2_off + grp) * HW + rem) * 16 + hk * 8,
+                                      G.out2_ps, v);
+                    }
+                }
+        }
+    }
+}
+
+// Stream-K fixup: grid (tiles, MT*PT/256/8); each thread finishes 4 consecutive channels (half
+// a group) of one pixel of a shared tile: partial slabs summed in k order (deterministic).
+template <int MT, int PT>
+__global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
+    const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
+    const int nK = a.nK;
+    const long long Gw = a.sk_grid;
+    const long long I = (long long)nM * nP * a.ngroups * nK;
+    const int tile = blockIdx.x;
+    const long long x0 = (long long)tile * nK;
+    const int w0 = (int)(((x0 + 1) * Gw - 1) / I);
+    const int w1 = (int)(((x0 + nK) * Gw - 1) / I);
+    if (w0 == w1) return;
+    const int mt = tile % nM;
+    const int rest = tile / nM;
+    const int pt = rest % nP;
+    const int g = rest / nP;
+    const X6Group G = g == 0 ? a.g[0] : a.g[1];
+    const int HW = a.H * a.W;
+    // thread -> (quad of channels, pixel); pixels fastest so slab reads stay coalesced
+    const int e = blockIdx.y * 256 + threadIdx.x;  // < MT/4 * PT
+    const int pl = e % PT, mq = e / PT;
+    const int ml0 = mq * 4;
+    const int mg = mt * MT + ml0;  // first channel of the quad
+    const int p = pt * PT + pl;
+    if (p >= a.npix) return;
+    const int cout8 = (G.cout + 7) & ~7;
+    if (mg >= (G.out_f32 ? G.cout : cout8)) return;
+    float v[4];
+    for (int w = w0; w <= w1; ++w) {
+        const long long lo_w = (long long)w * I / Gw;
+        const int slot = (lo_w / nK == tile) ? 2 * w : 2 * w + 1;
+        const float* s = a.partial + (size_t)slot * (MT * PT) + pl;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float x = s[(size_t)(ml0 + t) * PT];
+            v[t] = (w == w0) ? x : v[t] + x;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int m = mg + t;
+        v[t] += m < G.cout ? G.bias[m] : 0.f;
+        if (G.relu) v[t] = fmaxf(v[t], 0.f);
+    }
+    const int n = p / HW;
+    const int rem = p - n * HW;
+    if (G.out_f32) {
+        float* ob = static_cast<float*>(G.out) + ((size_t)n * G.out_c + G.out_off) * HW + rem;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (mg + t < G.cout) ob[(size_t)(mg + t) * HW] = v[t];
+        return;
+    }
+    const int grp = mg >> 3, half = (mg >> 2) & 1;
+    store4_x6(static_cast<uint8_t*>(G.out) + ((size_t)(n * G.out_c + G.out_off + grp) * HW + rem) * 16 + half * 8,
+              G.out_ps, v);
+    if (G.out2)
+        store4_x6(static_cast<uint8_t*>(G.out2) + ((size_t)(n * G.out2_c + G.out2_off + grp) * HW + rem) * 16 +
+                      half * 8,
+                  G.out2_ps, v);
+}
+
+// fp32 NCHW channels [coff, coff + C) of cstride -> X6 groups [goff, goff + ceil(C/8)) of cg
+// (channels >= C of the last group are written as 0)
+__global__ __launch_bounds__(256) void to_x6_kernel(const float* __restrict__ in, int cstride, int coff, int C, int N,
+                                                   int HW, uint8_t* __restrict__ out, int cg, int goff, uint32_t ps) {
+    const int G8 = (C + 7) / 8;
+    const size_t total = (size_t)N * G8 * HW;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int pix = (int)(e % HW);
+        const size_t t = e / HW;
+        const int gq = (int)(t % G8);
+        const int n = (int)(t / G8);
+        uint32_t h[3][8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int c = gq * 8 + k;
+            const float x = c < C ? in[((size_t)n * cstride + coff + c) * HW + pix] : 0.f;
+            split3(x, h[0][k], h[1][k], h[2][k]);
+        }
+        uint8_t* o = out + ((size_t)(n * cg + goff + gq) * HW + pix) * 16;
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+            uint4 w;
+            w.x = h[pc][0] | (h[pc][1] << 16);
+            w.y = h[pc][2] | (h[pc][3] << 16);
+            w.z = h[pc][4] | (h[pc][5] << 16);
+            w.w = h[pc][6] | (h[pc][7] << 16);
+            *reinterpret_cast<uint4*>(o + (size_t)pc * ps) = w;
+        }
+    }
+}
+
+// X6 groups -> fp32 NCHW channels [coff, coff + C) of cstride
+__global__ __launch_bounds__(256) void from_x6_kernel(const uint8_t* __restrict__ in, int cg, int goff, uint32_t ps,
+                                                     int C, int N, int HW, float* __restrict__ out, int cstride,
+                                                     int coff) {
+    const int G8 = (C + 7) / 8;
+    const size_t total = (size_t)N * G8 * HW;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int pix = (int)(e % HW);
+        const size_t t = e / HW;
+        const int gq = (int)(t % G8);
+        const int n = (int)(t / G8);
+        const uint8_t* s = in + ((size_t)(n * cg + goff + gq) * HW + pix) * 16;
+        const uint4 w0 = *reinterpret_cast<const uint4*>(s);
+        const uint4 w1 = *reinterpret_cast<const uint4*>(s + ps);
+        const uint4 w2 = *reinterpret_cast<const uint4*>(s + 2 * (size_t)ps);
+        const uint32_t a0[4] = {w0.x, w0.y, w0.z, w0.w}, a1[4] = {w1.x, w1.y, w1.z, w1.w},
+                       a2[4] = {w2.x, w2.y, w2.z, w2.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int c = gq * 8 + k;
+            if (c >= C) break;
+            const int sh = (k & 1) * 16;
+            const float x = join3((a0[k >> 1] >> sh) & 0xffffu, (a1[k >> 1] >> sh) & 0xffffu,
+                                  (a2[k >> 1] >> sh) & 0xffffu);
+            out[((size_t)n * cstride + coff + c) * HW + pix] = x;
+        }
+    }
+}
+
+// MaxPool2d(2, 2) floor mode (src/model.py:10-13) on X6: exact max of the rebuilt fp32 values
+__global__ __launch_bounds__(256) void maxpool_x6_kernel(const uint8_t* __restrict__ in, uint32_t ips,
+                                                        uint8_t* __restrict__ out, uint32_t ops, int NG, int H, int W) {
+    const int Ho = H >> 1, Wo = W >> 1;
+    const size_t total = (size_t)NG * Ho * Wo;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int x = (int)(e % Wo);
+        const size_t t = e / Wo;
+        const int y = (int)(t % Ho);
+        const size_t ng = t / Ho;
+        float m[8];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint8_t* s = in + ((ng * H + 2 * y + (d >> 1)) * W + 2 * x + (d & 1)) * 16;
+            const uint4 w0 = *reinterpret_cast<const uint4*>(s);
+            const uint4 w1 = *reinterpret_cast<const uint4*>(s + ips);
+            const uint4 w2 = *reinterpret_cast<const uint4*>(s + 2 * (size_t)ips);
+            const uint32_t a0[4] = {w0.x, w0.y, w0.z, w0.w}, a1[4] = {w1.x, w1.y, w1.z, w1.w},
+                           a2[4] = {w2.x, w2.y, w2.z, w2.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int sh = (k & 1) * 16;
+                const float v = join3((a0[k >> 1] >> sh) & 0xffffu, (a1[k >> 1] >> sh) & 0xffffu,
+                                      (a2[k >> 1] >> sh) & 0xffffu);
+                m[k] = d == 0 ? v : fmaxf(m[k], v);
+            }
+        }
+        uint32_t h[3][8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) split3(m[k], h[0][k], h[1][k], h[2][k]);
+        uint8_t* o = out + e * 16;
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+            uint4 w;
+            w.x = h[pc][0] | (h[pc][1] << 16);
+            w.y = h[pc][2] | (h[pc][3] << 16);
+            w.z = h[pc][4] | (h[pc][5] << 16);
+            w.w = h[pc][6] | (h[pc][7] << 16);
+            *reinterpret_cast<uint4*>(o + (size_t)pc * ops) = w;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ host side
+// weights [cout][cin][ks][ks] (fp32, physical input channel order) -> X6 chunks
+void x6_pack_weights(const float* w, int cout, int cin, int ks, int Mpad, int* nK_out, std::vector<uint16_t>& out) {
+    const int taps = ks * ks;
+    const int cin_g = (cin + 7) / 8;
+    const bool small = cin_g == 1;
+    const int nK = small ? (taps + 3) / 4 : ((cin_g + 3) / 4) * taps;
+    *nK_out = nK;
+    out.assign((size_t)nK * 12 * Mpad * 8, 0);
+    auto rne = [](float x) -> uint32_t {
+        uint32_t u;
+        std::memcpy(&u, &x, 4);
+        u += 0x7fffu + ((u >> 16) & 1u);
+        return u >> 16;
+    };
+    auto f = [](uint32_t h) {
+        const uint32_t u = h << 16;
+        float x;
+        std::memcpy(&x, &u, 4);
+        return x;
+    };
+    for (int c = 0; c < nK; ++c)
+        for (int gi = 0; gi < 4; ++gi) {
+            int tap, grp;
+            if (small) {
+                tap = c * 4 + gi;
+                grp = 0;
+            } else {
+                tap = c % taps;
+                grp = (c / taps) * 4 + gi;
+            }
+            for (int m = 0; m < cout; ++m)
+                for (int e = 0; e < 8; ++e) {
+                    const int ch = grp * 8 + e;
+                    if (tap >= taps || ch >= cin) continue;
+                    const float x = w[((size_t)m * cin + ch) * taps + tap];
+                    const uint32_t h0 = rne(x);
+                    const float r = x - f(h0);
+                    const uint32_t h1 = rne(r);
+                    const uint32_t h2 = rne(r - f(h1));
+                    const uint32_t hs[3] = {h0, h1, h2};
+                    for (int pc = 0; pc < 3; ++pc)
+                        out[(((size_t)c * 12 + pc * 4 + gi) * Mpad + m) * 8 + e] = (uint16_t)hs[pc];
+                }
+        }
+}
+
+template <int MT, int PT>
+static void launch_x6_tile(const X6Args& a, hipStream_t st) {
+    const bool small = a.small != 0;
+    if (small)
+        hipLaunchKernelGGL((conv_x6<MT, PT, true, 0>), dim3(a.sk_grid), dim3(64 * x6_waves(MT, PT)), 0, st, a);
+    else if (a.ks == 7)
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 7>), dim3(a.sk_grid), dim3(64 * x6_waves(MT, PT)), 0, st, a);
+    else if (a.ks == 3)
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 3>), dim3(a.sk_grid), dim3(64 * x6_waves(MT, PT)), 0, st, a);
+    else if (a.ks == 1)
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 1>), dim3(a.sk_grid), dim3(64 * x6_waves(MT, PT)), 0, st, a);
+    else
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 0>), dim3(a.sk_grid), dim3(64 * x6_waves(MT, PT)), 0, st, a);
+    const int tiles = (a.Mpad / MT) * ((a.npix + PT - 1) / PT) * a.ngroups;
+    if (a.sk_grid != tiles)
+        hipLaunchKernelGGL((conv_x6_fixup<MT, PT>), dim3(tiles, MT * PT / 4 / 256), dim3(256), 0, st, a);
+}
+
+void launch_conv_x6(const X6Args& a, int mt, int pt, hipStream_t st) {
+    if (mt == 128 && pt == 128) launch_x6_tile<128, 128>(a, st);
+    else if (mt == 128 && pt == 256) launch_x6_tile<128, 256>(a, st);
+    else if (mt == 256 && pt == 128) launch_x6_tile<256, 128>(a, st);
+    else if (mt == 128 && pt == 64) launch_x6_tile<128, 64>(a, st);
+    else if (mt == 64 && pt == 128) launch_x6_tile<64, 128>(a, st);
+    else if (mt == 64 && pt == 64) launch_x6_tile<64, 64>(a, st);
+    else throw std::invalid_argument("unsupported x6 conv tile");
+}
+
+static int grid_for(size_t total) {
+    size_t b = (total + 255) / 256;
+    return (int)(b > 8192 ? 8192 : (b ? b : 1));
+}
+
+void launch_to_x6(const float* in, int cstride, int coff, int C, int N, int HW, uint8_t* out, int cg, int goff,
+                  uint32_t ps, hipStream_t st) {
+    hipLaunchKernelGGL(to_x6_kernel, dim3(grid_for((size_t)N * ((C + 7) / 8) * HW)), dim3(256), 0, st, in, cstride,
+                       coff, C, N, HW, out, cg, goff, ps);
+}
+
+void launch_from_x6(const uint8_t* in, int cg, int goff, uint32_t ps, int C, int N, int HW, float* out, int cstride,
+                    int coff, hipStream_t st) {
+    hipLaunchKernelGGL(from_x6_kernel, dim3(grid_for((size_t)N * ((C + 7) / 8) * HW)), dim3(256), 0, st, in, cg,
+                       goff, ps, C, N, HW, out, cstride, coff);
+}
+
+void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(maxpool_x6_kernel, dim3(grid_for((size_t)NG * (H / 2) * (W / 2))), dim3(256), 0, st, in, ips,
+                       out, ops, NG, H, W);
+}
+
+}  // namespace opose

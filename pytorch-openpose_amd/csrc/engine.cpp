@@ -129,7 +129,13 @@ struct DevConv {
     float* wt = nullptr;
     float* bias = nullptr;
     int* ktab = nullptr;
+    // split-bf16 (X6) form: [nK6][3][4][Mpad] units of 8 bf16, input channels in the physical
+    // (group-aligned) order of the X6 activation buffers; see conv_x6.hip
+    uint8_t* wx6 = nullptr;
+    int nK6 = 0, cin_g = 0;
+    bool small6 = false;
     ~DevConv() {
+        if (wx6) (void)hipFree(wx6);
         if (wt) (void)hipFree(wt);
         if (bias) (void)hipFree(bias);
         if (ktab) (void)hipFree(ktab);
@@ -178,6 +184,14 @@ struct opose_ctx {
     std::map<std::string, std::unique_ptr<DevConv>> convs[2];
     bool loaded[2] = {false, false};
     // workspace
+    // split-bf16 (X6) activations of the x6 network path (conv_x6.hip)
+    DevBuf x6in, x6A, x6B, x6S0, x6S1, x6T0, x6T1, x6U;
+    // network convolutions: fp32-accurate split-bf16 kernel (default) or the fp32 MFMA kernel
+    // (OPOSE_CONV=f32)
+    bool x6 = [] {
+        const char* e = getenv("OPOSE_CONV");
+        return !(e && std::string(e) == "f32");
+    }();
     DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[kMaxScales], avg, cnt, list, peak_pos, part_cnt,
         score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score, skcnt, hsel;
     // stream-K: split tiles reduced by the conv_sk_fixup launch (default) or in-kernel by the
@@ -266,9 +280,13 @@ struct TileChoice {
 // holds k >= 2 co-resident workgroups finishes them in k * work; a lone workgroup (one wave per
 // SIMD) runs at ~60 %.  Stream-K (grid = all resident slots) balances the chip exactly and
 // pays for the partial slabs of tiles it splits plus one fixup launch.
-TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK) {
+TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false) {
     static const int cfg[6][3] = {{128, 128, 2}, {128, 256, 1}, {256, 128, 1},
                                   {128, 64, 3},  {64, 128, 3},  {64, 64, 4}};  // mt, pt, WG/CU
+    // split-bf16 kernel: 2.5x the MFMA rate per chunk, more LDS per workgroup
+    static const int occ6[6] = {1, 1, 1, 2, 2, 3};
+    static const double ovh6[6] = {1.5, 1.0, 1.0, 1.1, 1.1, 1.2};
+    const double rate = x6 ? 0.4 : 1.0;
     // relative cost per MFMA of the smaller tiles (more load/issue work per MFMA); measured
     // with scripts/conv_timing.py, overridable for A/B runs: OPOSE_TILE_OVH="1,.95,.93,1.02,1.02,1.06"
     static double ovh[6] = {1.0, 0.95, 0.93, 1.02, 1.02, 1.06};
@@ -281,10 +299,10 @@ TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK) {
     TileChoice best{64, 64, 1};
     double best_cost = 1e300;
     for (int c = 0; c < 6; ++c) {
-        const int mt = cfg[c][0], pt = cfg[c][1], occ = cfg[c][2];
+        const int mt = cfg[c][0], pt = cfg[c][1], occ = x6 ? occ6[c] : cfg[c][2];
         if (Mpad % mt) continue;
         const long tiles = (long)(Mpad / mt) * ((npix + pt - 1) / pt) * ngroups;
-        const double unit = (mt / 64.0) * (pt / 64.0) * ovh[c];
+        const double unit = (mt / 64.0) * (pt / 64.0) * (x6 ? ovh6[c] : ovh[c]) * rate;
         // data parallel
         const long per_cu = (tiles + 255) / 256;
         // one resident workgroup of a 2-per-CU config runs at ~60 % (floor 1.6); the 8-wave
@@ -332,7 +350,8 @@ static DevConv* find_conv(opose_ctx* h, int net, const std::string& name) {
 }
 
 static void upload_conv(opose_ctx* h, int net, const std::string& key, const std::vector<const Spec*>& parts,
-                        const std::vector<const float*>& w, const std::vector<const float*>& b) {
+                        const std::vector<const float*>& w, const std::vector<const float*>& b,
+                        const std::vector<int>& cmap = {}) {
     auto dc = std::make_unique<DevConv>();
     const Spec& s0 = *parts[0];
     dc->name = key;
@@ -368,6 +387,26 @@ static void upload_conv(opose_ctx* h, int net, const std::string& key, const std
     for (int k = 0; k < dc->K; ++k) {
         int c = k / (dc->ks * dc->ks), r = k % (dc->ks * dc->ks);
         ktab[k] = (c << 8) | ((r / dc->ks) << 4) | (r % dc->ks);
+    }
+    // X6 weights: input channel c of the reference layer sits at physical channel cmap[c]
+    {
+        const int cin_phys = cmap.empty() ? s0.cin : cmap.back() + 1;
+        const int taps = s0.ks * s0.ks;
+        std::vector<float> wp((size_t)cout * cin_phys * taps, 0.f);
+        int mm = 0;
+        for (size_t i = 0; i < parts.size(); ++i)
+            for (int m = 0; m < parts[i]->cout; ++m, ++mm)
+                for (int c = 0; c < s0.cin; ++c) {
+                    const int pc = cmap.empty() ? c : cmap[c];
+                    for (int t = 0; t < taps; ++t)
+                        wp[((size_t)mm * cin_phys + pc) * taps + t] = w[i][((size_t)m * s0.cin + c) * taps + t];
+                }
+        std::vector<uint16_t> wx;
+        x6_pack_weights(wp.data(), cout, cin_phys, s0.ks, dc->Mpad, &dc->nK6, wx);
+        dc->cin_g = (cin_phys + 7) / 8;
+        dc->small6 = dc->cin_g == 1;
+        OPOSE_HIP_CHECK(hipMalloc(&dc->wx6, wx.size() * 2));
+        OPOSE_HIP_CHECK(hipMemcpy(dc->wx6, wx.data(), wx.size() * 2, hipMemcpyHostToDevice));
     }
     OPOSE_HIP_CHECK(hipMalloc(&dc->wt, wt.size() * 4));
     OPOSE_HIP_CHECK(hipMalloc(&dc->bias, bias.size() * 4));
@@ -475,9 +514,203 @@ static void run_trunk(opose_ctx* h, int net, const float* x, int N, int H, int W
     }
 }
 
+// ---------------------------------------------------------------- split-bf16 network path
+struct XAct {  // a group slice of an X6 buffer (or, f32: a channel slice of an fp32 NCHW buffer)
+    void* p = nullptr;
+    int c = 0, off = 0;  // X6: groups per frame / first group; f32: channels / first channel
+    uint32_t ps = 0;     // X6 piece stride (bytes)
+    bool f32 = false;
+};
+
+static XAct x6act(uint8_t* p, int cg, int goff, size_t npix) {
+    const size_t ps = npix * (size_t)cg * 16;
+    if (ps * 3 >= 2147483648.0) throw std::invalid_argument("X6 activation >= 2 GiB: split the batch");
+    return XAct{p, cg, goff, (uint32_t)ps, false};
+}
+
+static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W, XAct in0, XAct out0, XAct in1,
+                        XAct out1, bool relu0, bool relu1, XAct dup = XAct{}) {
+    X6Args a{};
+    const int ng = c1 ? 2 : 1;
+    a.N = N;
+    a.H = H;
+    a.W = W;
+    a.ks = c0->ks;
+    a.pad = c0->pad;
+    a.cin_g = c0->cin_g;
+    a.small = c0->small6 ? 1 : 0;
+    a.nK = c0->nK6;
+    a.Mpad = c0->Mpad;
+    a.npix = N * H * W;
+    DevConv* cs[2] = {c0, c1};
+    XAct ins[2] = {in0, in1}, outs[2] = {out0, out1};
+    bool relus[2] = {relu0, relu1};
+    for (int g = 0; g < ng; ++g) {
+        X6Group& G = a.g[g];
+        G.in = static_cast<const uint8_t*>(ins[g].p);
+        G.in_ps = ins[g].ps;
+        G.in_cg = ins[g].c;
+        G.in_goff = ins[g].off;
+        G.wt = cs[g]->wx6;
+        G.bias = cs[g]->bias;
+        G.out = outs[g].p;
+        G.out_ps = outs[g].ps;
+        G.out_c = outs[g].c;
+        G.out_off = outs[g].off;
+        G.out_f32 = outs[g].f32 ? 1 : 0;
+        G.out2 = nullptr;
+        G.cout = cs[g]->cout;
+        G.relu = relus[g] ? 1 : 0;
+    }
+    if (dup.p) {
+        a.g[0].out2 = dup.p;
+        a.g[0].out2_ps = dup.ps;
+        a.g[0].out2_c = dup.c;
+        a.g[0].out2_off = dup.off;
+    }
+    if (ng == 1) a.g[1] = a.g[0];
+    const TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.nK, true);
+    a.ngroups = ng;
+    a.sk_grid = t.grid;
+    a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+    double flops = 0;
+    for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)c0->K * a.npix;
+    ProfEntry pe;
+    h->prof_begin(pe, conv_class(c0->ks), flops, 0);
+    if (h->detail)
+        pe.detail = "layer/" + c0->name + "/x6/" + std::to_string(t.mt) + "x" + std::to_string(t.pt) + "s" +
+                    std::to_string(t.grid) + "/n" + std::to_string(a.npix);
+    launch_conv_x6(a, t.mt, t.pt, h->stream);
+    h->prof_end(pe);
+}
+
+// VGG trunk on X6 activations: x fp32 [N,3,H,W] -> final trunk conv written via `last` (+ dup)
+static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, int W, XAct last, XAct dup) {
+    const std::vector<Spec> vgg = net == OPOSE_NET_BODY ? vgg_body() : vgg_hand();
+    const size_t npix = (size_t)N * H * W;
+    uint8_t* X = h->x6in.ensure<uint8_t>(npix * 16 * 3, h->stream);
+    {
+        ProfEntry pe;
+        h->prof_begin(pe, "to_x6", 0, (double)npix * (12 + 48));
+        launch_to_x6(x, 3, 0, 3, N, H * W, X, 1, 0, (uint32_t)(npix * 16), h->stream);
+        h->prof_end(pe);
+    }
+    const size_t act = npix * 8 * 16 * 3;  // 64 channels at full resolution = the largest trunk tensor
+    uint8_t* A = h->x6A.ensure<uint8_t>(act, h->stream);
+    uint8_t* B = h->x6B.ensure<uint8_t>(act, h->stream);
+    uint8_t* cur = X;
+    int cg = 1, hh = H, ww = W;
+    for (size_t i = 0; i < vgg.size(); ++i) {
+        const Spec& s = vgg[i];
+        DevConv* c = find_conv(h, net, s.name);
+        const bool final_layer = i + 1 == vgg.size();
+        uint8_t* dst = (cur == A) ? B : A;
+        const int og = (s.cout + 7) / 8;
+        const size_t np = (size_t)N * hh * ww;
+        XAct out = final_layer ? last : x6act(dst, og, 0, np);
+        run_conv_x6(h, c, nullptr, N, hh, ww, x6act(cur, cg, 0, np), out, XAct{}, XAct{}, true, false,
+                    final_layer ? dup : XAct{});
+        cur = dst;
+        cg = og;
+        if (s.name == "conv1_2" || s.name == "conv2_2" || s.name == "conv3_4") {
+            uint8_t* pd = (cur == A) ? B : A;
+            ProfEntry pe;
+            h->prof_begin(pe, "maxpool", 0, (double)np * cg * 48 * 1.25);
+            launch_maxpool_x6(cur, (uint32_t)(np * cg * 16), pd, (uint32_t)((size_t)N * (hh / 2) * (ww / 2) * cg * 16),
+                              N * cg, hh, ww, h->stream);
+            h->prof_end(pe);
+            hh /= 2;
+            ww /= 2;
+            cur = pd;
+        }
+    }
+}
+
+// bodypose_model.forward on X6 activations; output fp32 in S0 with the fp32 path's layout
+// (channel stride 185: paf [0,38), heat [38,57))
+static float* body_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
+    const int hl = Hp / 8, wl = Wp / 8;
+    const size_t px = (size_t)N * hl * wl;
+    const int SG = 24, TG = 32, UG = 128;  // [L1 | L2 | trunk] = 5 + 3 + 16 groups; 256 / 1024 channels
+    uint8_t* S[2] = {h->x6S0.ensure<uint8_t>(px * SG * 48, h->stream), h->x6S1.ensure<uint8_t>(px * SG * 48, h->stream)};
+    uint8_t* T[2] = {h->x6T0.ensure<uint8_t>(px * TG * 48, h->stream), h->x6T1.ensure<uint8_t>(px * TG * 48, h->stream)};
+    uint8_t* U = h->x6U.ensure<uint8_t>(px * UG * 48, h->stream);
+    float* O = h->S0.ensure<float>(px * 185, h->stream);
+    const int net = OPOSE_NET_BODY;
+    auto s_ = [&](int i, int goff) { return x6act(S[i], SG, goff, px); };
+    auto t_ = [&](int i, int goff) { return x6act(T[i], TG, goff, px); };
+    auto u_ = [&](int goff) { return x6act(U, UG, goff, px); };
+    run_trunk_x6(h, net, x, N, Hp, Wp, s_(0, 8), s_(1, 8));
+    run_conv_x6(h, find_conv(h, net, "conv5_1_CPM_L1+L2"), nullptr, N, hl, wl, s_(0, 8), t_(0, 0), XAct{}, XAct{},
+                true, false);
+    run_conv_x6(h, find_conv(h, net, "conv5_2_CPM_L1"), find_conv(h, net, "conv5_2_CPM_L2"), N, hl, wl, t_(0, 0),
+                t_(1, 0), t_(0, 16), t_(1, 16), true, true);
+    run_conv_x6(h, find_conv(h, net, "conv5_3_CPM_L1"), find_conv(h, net, "conv5_3_CPM_L2"), N, hl, wl, t_(1, 0),
+                t_(0, 0), t_(1, 16), t_(0, 16), true, true);
+    run_conv_x6(h, find_conv(h, net, "conv5_4_CPM_L1"), find_conv(h, net, "conv5_4_CPM_L2"), N, hl, wl, t_(0, 0),
+                u_(0), t_(0, 16), u_(64), true, true);
+    run_conv_x6(h, find_conv(h, net, "conv5_5_CPM_L1"), find_conv(h, net, "conv5_5_CPM_L2"), N, hl, wl, u_(0),
+                s_(1, 0), u_(64), s_(1, 5), false, false);
+    int cur = 1;
+    for (int st = 2; st <= 6; ++st) {
+        const std::string sf = "_stage" + std::to_string(st);
+        run_conv_x6(h, find_conv(h, net, "Mconv1" + sf + "_L1+L2"), nullptr, N, hl, wl, s_(cur, 0), t_(0, 0),
+                    XAct{}, XAct{}, true, false);
+        int t = 0;
+        for (int i = 2; i <= 6; ++i) {
+            const std::string nm = "Mconv" + std::to_string(i) + sf;
+            run_conv_x6(h, find_conv(h, net, nm + "_L1"), find_conv(h, net, nm + "_L2"), N, hl, wl, t_(t, 0),
+                        t_(t ^ 1, 0), t_(t, 16), t_(t ^ 1, 16), true, true);
+            t ^= 1;
+        }
+        const XAct o1 = st == 6 ? XAct{O, 185, 0, 0, true} : s_(cur ^ 1, 0);
+        const XAct o2 = st == 6 ? XAct{O, 185, 38, 0, true} : s_(cur ^ 1, 5);
+        run_conv_x6(h, find_conv(h, net, "Mconv7" + sf + "_L1"), find_conv(h, net, "Mconv7" + sf + "_L2"), N, hl, wl,
+                    t_(t, 0), o1, t_(t, 16), o2, false, st == 6);
+        cur ^= 1;
+    }
+    return O;
+}
+
+// handpose_model.forward on X6 activations; output fp32 in S0, channel stride 150 (heat [0,22))
+static float* hand_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
+    const int hl = Hp / 8, wl = Wp / 8;
+    const size_t px = (size_t)N * hl * wl;
+    const int SG = 19, TG = 16, UG = 64;  // [L 22 + 2 | trunk 128] = 3 + 16 groups; 128 / 512 channels
+    uint8_t* S[2] = {h->x6S0.ensure<uint8_t>(px * SG * 48, h->stream), h->x6S1.ensure<uint8_t>(px * SG * 48, h->stream)};
+    uint8_t* T[2] = {h->x6T0.ensure<uint8_t>(px * TG * 48, h->stream), h->x6T1.ensure<uint8_t>(px * TG * 48, h->stream)};
+    uint8_t* U = h->x6U.ensure<uint8_t>(px * UG * 48, h->stream);
+    float* O = h->S0.ensure<float>(px * 150, h->stream);
+    const int net = OPOSE_NET_HAND;
+    auto s_ = [&](int i, int goff) { return x6act(S[i], SG, goff, px); };
+    auto t_ = [&](int i) { return x6act(T[i], TG, 0, px); };
+    run_trunk_x6(h, net, x, N, Hp, Wp, s_(0, 3), s_(1, 3));
+    run_conv_x6(h, find_conv(h, net, "conv6_1_CPM"), nullptr, N, hl, wl, s_(0, 3), x6act(U, UG, 0, px), XAct{},
+                XAct{}, true, false);
+    run_conv_x6(h, find_conv(h, net, "conv6_2_CPM"), nullptr, N, hl, wl, x6act(U, UG, 0, px), s_(1, 0), XAct{},
+                XAct{}, false, false);
+    int cur = 1;
+    for (int st = 2; st <= 6; ++st) {
+        const std::string sf = "_stage" + std::to_string(st);
+        run_conv_x6(h, find_conv(h, net, "Mconv1" + sf), nullptr, N, hl, wl, s_(cur, 0), t_(0), XAct{}, XAct{}, true,
+                    false);
+        int t = 0;
+        for (int i = 2; i <= 6; ++i) {
+            run_conv_x6(h, find_conv(h, net, "Mconv" + std::to_string(i) + sf), nullptr, N, hl, wl, t_(t), t_(t ^ 1),
+                        XAct{}, XAct{}, true, false);
+            t ^= 1;
+        }
+        const XAct o = st == 6 ? XAct{O, 150, 0, 0, true} : s_(cur ^ 1, 0);
+        run_conv_x6(h, find_conv(h, net, "Mconv7" + sf), nullptr, N, hl, wl, t_(t), o, XAct{}, XAct{}, false, false);
+        cur ^= 1;
+    }
+    return O;
+}
+
 // bodypose_model.forward (src/model.py:106-133). Output: S-buffer with paf [0,38), heat [38,57)
 static float* body_net(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
     if (!h->loaded[OPOSE_NET_BODY]) throw std::runtime_error("body weights not loaded");
+    if (h->x6) return body_net_x6(h, x, N, Hp, Wp);
     const int hl = Hp / 8, wl = Wp / 8;
     const size_t px = (size_t)N * hl * wl;
     float* S[2] = {h->S0.ensure<float>(px * 185, h->stream), h->S1.ensure<float>(px * 185, h->stream)};
@@ -521,6 +754,7 @@ static float* body_net(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
 // handpose_model.forward (src/model.py:197-214). Output: S-buffer with heat [0,22)
 static float* hand_net(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
     if (!h->loaded[OPOSE_NET_HAND]) throw std::runtime_error("hand weights not loaded");
+    if (h->x6) return hand_net_x6(h, x, N, Hp, Wp);
     const int hl = Hp / 8, wl = Wp / 8;
     const size_t px = (size_t)N * hl * wl;
     float* S[2] = {h->S0.ensure<float>(px * 150, h->stream), h->S1.ensure<float>(px * 150, h->stream)};
@@ -871,8 +1105,16 @@ int opose_load_weights(opose_t* h, int net, const float* const* tensors, const i
             byname[s.name] = {tensors[2 * i], tensors[2 * i + 1]};
         }
         h->convs[net].clear();
+        // physical channel order of the X6 stage-input concat (8-channel groups): body
+        // [L1 38 | pad 2 | L2 19 | pad 5 | trunk 128], hand [L 22 | pad 2 | trunk 128]
+        std::vector<int> cmap;
+        if (net == OPOSE_NET_BODY)
+            for (int c = 0; c < 185; ++c) cmap.push_back(c < 38 ? c : (c < 57 ? c + 2 : c + 7));
+        else
+            for (int c = 0; c < 150; ++c) cmap.push_back(c < 22 ? c : c + 2);
         for (const Spec& s : order)
-            upload_conv(h, net, s.name, {&s}, {byname[s.name].first}, {byname[s.name].second});
+            upload_conv(h, net, s.name, {&s}, {byname[s.name].first}, {byname[s.name].second},
+                        s.name.rfind("Mconv1_", 0) == 0 ? cmap : std::vector<int>{});
         if (net == OPOSE_NET_BODY) {
             // branch-pair layers sharing an input become one GEMM with M = 256
             std::vector<std::string> shared = {"conv5_1_CPM"};
@@ -885,7 +1127,8 @@ int opose_load_weights(opose_t* h, int net, const float* const* tensors, const i
                     if (s.name == l2) s2 = &s;
                 }
                 upload_conv(h, net, base + "_L1+L2", {s1, s2}, {byname[l1].first, byname[l2].first},
-                            {byname[l1].second, byname[l2].second});
+                            {byname[l1].second, byname[l2].second},
+                            base.rfind("Mconv1_", 0) == 0 ? cmap : std::vector<int>{});
             }
         }
         h->loaded[net] = true;
@@ -1468,6 +1711,107 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
         OPOSE_HIP_CHECK(hipMemcpyAsync(out, yd, ny * 4, hipMemcpyDeviceToHost, h->stream));
         OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
         h->convs[0].erase("__debug__");
+    });
+    return OPOSE_OK;
+}
+
+// split-bf16 conv of one layer: x fp32 NCHW -> X6 -> conv_x6 -> fp32 (out_x6: through an X6
+// output buffer and back, exercising the split epilogue)
+int opose_debug_conv_x6(opose_t* h, const float* x, const float* w, const float* b, int N, int Cin, int H, int W,
+                        int Cout, int ks, int pad, int relu, int mt, int pt, int splits, int out_x6, float* out) {
+    if (!h || !x || !w || !b || !out || ks > 15 || pad > 7) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        Spec s{"debug", Cin, Cout, ks, pad};
+        upload_conv(h, 0, "__debug__", {&s}, {w}, {b});
+        DevConv* c = h->convs[0]["__debug__"].get();
+        const int HW = H * W;
+        const int cg = c->cin_g, og = (Cout + 7) / 8;
+        DevBuf xin, xx, yx, yout;
+        const size_t nx = (size_t)N * Cin * HW, ny = (size_t)N * Cout * HW;
+        const uint32_t ips = (uint32_t)((size_t)N * cg * HW * 16), ops = (uint32_t)((size_t)N * og * HW * 16);
+        float* xd = xin.ensure<float>(nx, h->stream);
+        uint8_t* x6 = xx.ensure<uint8_t>((size_t)ips * 3, h->stream);
+        uint8_t* y6 = yx.ensure<uint8_t>((size_t)ops * 3, h->stream);
+        float* yd = yout.ensure<float>(ny, h->stream);
+        OPOSE_HIP_CHECK(hipMemcpyAsync(xd, x, nx * 4, hipMemcpyHostToDevice, h->stream));
+        launch_to_x6(xd, Cin, 0, Cin, N, HW, x6, cg, 0, ips, h->stream);
+        X6Args a{};
+        a.N = N; a.H = H; a.W = W; a.ks = ks; a.pad = pad;
+        a.cin_g = cg; a.small = c->small6 ? 1 : 0; a.nK = c->nK6; a.Mpad = c->Mpad; a.npix = N * HW;
+        X6Group& G = a.g[0];
+        G.in = x6; G.in_ps = ips; G.in_cg = cg; G.in_goff = 0;
+        G.wt = c->wx6; G.bias = c->bias; G.cout = Cout; G.relu = relu; G.out2 = nullptr;
+        if (out_x6) { G.out = y6; G.out_ps = ops; G.out_c = og; G.out_off = 0; G.out_f32 = 0; }
+        else { G.out = yd; G.out_c = Cout; G.out_off = 0; G.out_f32 = 1; }
+        a.g[1] = a.g[0];
+        TileChoice t = choose_tile(a.Mpad, a.npix, 1, a.nK, true);
+        if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((a.npix + pt - 1) / pt); }
+        if (splits > 0) t.grid = splits;
+        if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
+        a.ngroups = 1;
+        a.sk_grid = t.grid;
+        a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        launch_conv_x6(a, t.mt, t.pt, h->stream);
+        if (out_x6) launch_from_x6(y6, og, 0, ops, Cout, N, HW, yd, Cout, 0, h->stream);
+        OPOSE_HIP_CHECK(hipMemcpyAsync(out, yd, ny * 4, hipMemcpyDeviceToHost, h->stream));
+        OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+        h->convs[0].erase("__debug__");
+    });
+    return OPOSE_OK;
+}
+
+// timing of one split-bf16 conv launch configuration on hashed data
+int opose_debug_conv_x6_time(opose_t* h, int N, int Cin, int H, int W, int Cout, int ks, int ngroups, int mt, int pt,
+                             int splits, int reps, float* ms) {
+    if (!h || !ms || reps < 1 || ngroups < 1 || ngroups > 2) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        Spec s{"timing", Cin, Cout, ks, ks / 2};
+        std::vector<float> w((size_t)Cout * Cin * ks * ks), b(Cout, 0.f);
+        for (size_t i = 0; i < w.size(); ++i) w[i] = (float)((i * 2654435761u) % 2001) / 1000.f - 1.f;
+        upload_conv(h, 0, "__timing__", {&s}, {w.data()}, {b.data()});
+        DevConv* c = h->convs[0]["__timing__"].get();
+        const int HW = H * W;
+        const int cg = c->cin_g, og = (Cout + 7) / 8;
+        const uint32_t ips = (uint32_t)((size_t)ngroups * N * cg * HW * 16);
+        const uint32_t ops = (uint32_t)((size_t)ngroups * N * og * HW * 16);
+        DevBuf xin, xx, yx;
+        float* xd = xin.ensure<float>((size_t)ngroups * N * cg * 8 * HW, h->stream);
+        launch_fill_hash(xd, (size_t)ngroups * N * cg * 8 * HW, 0x80000003u, h->stream);
+        uint8_t* x6 = xx.ensure<uint8_t>((size_t)ips * 3, h->stream);
+        uint8_t* y6 = yx.ensure<uint8_t>((size_t)ops * 3, h->stream);
+        launch_to_x6(xd, cg * 8, 0, cg * 8, ngroups * N, HW, x6, cg, 0, ips, h->stream);
+        X6Args a{};
+        a.N = N; a.H = H; a.W = W; a.ks = ks; a.pad = ks / 2;
+        a.cin_g = cg; a.small = c->small6 ? 1 : 0; a.nK = c->nK6; a.Mpad = c->Mpad; a.npix = N * HW;
+        for (int g = 0; g < 2; ++g) {
+            X6Group& G = a.g[g];
+            const int gg = g < ngroups ? g : 0;
+            G.in = x6 + (size_t)gg * N * cg * HW * 16; G.in_ps = ips; G.in_cg = cg; G.in_goff = 0;
+            G.wt = c->wx6; G.bias = c->bias; G.cout = Cout; G.relu = 1; G.out2 = nullptr;
+            G.out = y6 + (size_t)gg * N * og * HW * 16; G.out_ps = ops; G.out_c = og; G.out_off = 0; G.out_f32 = 0;
+        }
+        TileChoice t = choose_tile(a.Mpad, a.npix, ngroups, a.nK, true);
+        if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((a.npix + pt - 1) / pt) * ngroups; }
+        if (splits > 0) t.grid = splits;
+        if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
+        a.ngroups = ngroups;
+        a.sk_grid = t.grid;
+        a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        launch_conv_x6(a, t.mt, t.pt, h->stream);  // warm-up
+        hipEvent_t e0, e1;
+        OPOSE_HIP_CHECK(hipEventCreate(&e0));
+        OPOSE_HIP_CHECK(hipEventCreate(&e1));
+        OPOSE_HIP_CHECK(hipEventRecord(e0, h->stream));
+        for (int r = 0; r < reps; ++r) launch_conv_x6(a, t.mt, t.pt, h->stream);
+        OPOSE_HIP_CHECK(hipEventRecord(e1, h->stream));
+        OPOSE_HIP_CHECK(hipEventSynchronize(e1));
+        OPOSE_HIP_CHECK(hipEventElapsedTime(ms, e0, e1));
+        *ms /= reps;
+        OPOSE_HIP_CHECK(hipEventDestroy(e0));
+        OPOSE_HIP_CHECK(hipEventDestroy(e1));
+        h->convs[0].erase("__timing__");
     });
     return OPOSE_OK;
 }

@@ -1,5 +1,7 @@
 // kernels.h — host-side launchers for the libopose kernels.
 #pragma once
+#include <vector>
+
 #include "common.h"
 
 namespace opose {
@@ -28,6 +30,16 @@ void launch_conv(const ConvArgs& a, const int* ktab, int mt, int pt, hipStream_t
 void launch_conv_ablation(const ConvArgs& a, int ablate, hipStream_t st);
 void launch_fill_hash(float* p, size_t n, uint32_t seed, hipStream_t st);
 void launch_maxpool(const float* in, float* out, int NC, int H, int W, hipStream_t st);
+
+// conv_x6.hip (split-bf16 fp32-accurate convolution, X6 activation format: common.h)
+void x6_pack_weights(const float* w, int cout, int cin, int ks, int Mpad, int* nK_out, std::vector<uint16_t>& out);
+void launch_conv_x6(const X6Args& a, int mt, int pt, hipStream_t st);
+void launch_to_x6(const float* in, int cstride, int coff, int C, int N, int HW, uint8_t* out, int cg, int goff,
+                  uint32_t ps, hipStream_t st);
+void launch_from_x6(const uint8_t* in, int cg, int goff, uint32_t ps, int C, int N, int HW, float* out, int cstride,
+                    int coff, hipStream_t st);
+void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,
+                       hipStream_t st);
 
 // imgproc.hip
 void launch_preprocess(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int Hs,

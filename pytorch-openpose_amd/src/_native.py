@@ -63,6 +63,8 @@ def _load():
         "opose_debug_conv": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P]),
         "opose_debug_preprocess": (I, [P, P, I, I, D, I, P, P]),
         "opose_debug_conv_time": (I, [P, I, I, I, I, I, I, I, I, I, I, I, I, P]),
+        "opose_debug_conv_x6": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P]),
+        "opose_debug_conv_x6_time": (I, [P, I, I, I, I, I, I, I, I, I, I, I, P]),
         "opose_debug_heat": (I, [P, P, I, I, I, I, I, I, P, P]),
     }
     for name, (res, args) in sig.items():
@@ -80,7 +82,7 @@ EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last
             "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_body_infer",
             "opose_body_post", "opose_body_scale_geom", "opose_body_scale_maps",
             "opose_body_post_scales", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
-            "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_conv_time", "opose_debug_preprocess",
+            "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_conv_time", "opose_debug_conv_x6", "opose_debug_conv_x6_time", "opose_debug_preprocess",
             "opose_debug_heat"]
 
 

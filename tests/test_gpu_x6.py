@@ -1,0 +1,114 @@
+"""GPU: the split-bf16 ("x6") convolution that runs the network by default (csrc/conv_x6.hip).
+
+Every fp32 operand is carried as three bf16 pieces (exact) and each product is rebuilt from
+six bf16 MFMA piece products; the claim is fp32 accuracy.  Tolerances:
+* single convs against a float64 reference: |err| <= 4e-6 * conv(|x|, |w|) + 1e-6 — the bound
+  the fp32 MFMA kernel is held to (tests/test_gpu_parity.py) — and the mean relative error
+  within 3x the fp32 kernel's on the same inputs;
+* the X6 epilogue (split store) + rebuild is lossless: identical to the fp32-output epilogue;
+* the whole network on the x6 path vs the fp32 MFMA path (OPOSE_CONV=f32): within the
+  network tolerance of test_gpu_parity (2e-4 * max|ref| + 2e-4 * |ref|); the e2e golden
+  fixtures of the reference (test_gpu_parity / test_gpu_pipeline) run on the x6 path too.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def native():
+    from src import _native
+    return _native
+
+
+@pytest.fixture(scope="module")
+def handle(native):
+    return native.Handle(0)
+
+
+def _run(native, handle, fn, x, w, b, relu, mt, pt, splits, *extra):
+    N, Cin, H, W = x.shape
+    Cout, _, ks, _ = w.shape
+    out = np.empty((N, Cout, H, W), np.float32)
+    handle.check(fn(handle.h, x.ctypes.data, w.ctypes.data, b.ctypes.data, N, Cin, H, W, Cout, ks, ks // 2,
+                    int(relu), mt, pt, splits, *extra, out.ctypes.data))
+    return out
+
+
+CASES = [
+    (1, 3, 40, 72, 64, 3, 0, 0, 0),          # conv1_1: one channel group, chunks of 4 taps
+    (2, 64, 20, 24, 96, 3, 0, 0, 0),         # Mpad 128 > Cout
+    (2, 128, 23, 41, 128, 7, 128, 256, 0),   # 8-wave tile, data parallel
+    (2, 128, 23, 41, 256, 7, 256, 128, 0),
+    (2, 185, 17, 19, 128, 7, 128, 128, 0),   # ragged channel groups (185 -> 24 groups, clamped reads)
+    (3, 64, 30, 33, 128, 3, 128, 64, 37),    # stream-K: partial slabs + fixup
+    (2, 96, 23, 41, 128, 3, 64, 128, 300),   # stream-K, more workgroups than tiles
+    (2, 128, 17, 19, 38, 1, 64, 64, 0),      # 1x1, Cout 38 (PAF head)
+    (1, 150, 9, 13, 128, 7, 64, 64, 5),      # hand Mconv1-like, tiny frame, 5 workgroups
+]
+
+
+@pytest.mark.parametrize("N,Cin,H,W,Cout,ks,mt,pt,splits", CASES)
+def test_x6_conv_fp32_accuracy(native, handle, N, Cin, H, W, Cout, ks, mt, pt, splits):
+    rng = np.random.default_rng(Cin * 7 + ks)
+    x = np.maximum(rng.standard_normal((N, Cin, H, W), dtype=np.float32), 0)  # post-ReLU activations
+    w = (rng.standard_normal((Cout, Cin, ks, ks), dtype=np.float32) * np.float32(np.sqrt(2 / (Cin * ks * ks))))
+    b = rng.standard_normal(Cout, dtype=np.float32) * np.float32(0.1)
+    y6 = _run(native, handle, native.lib.opose_debug_conv_x6, x, w, b, True, mt, pt, splits, 0)
+    y6x = _run(native, handle, native.lib.opose_debug_conv_x6, x, w, b, True, mt, pt, splits, 1)
+    y32 = _run(native, handle, native.lib.opose_debug_conv, x, w, b, True, mt, pt, splits)
+    xd, wd, bd = (torch.from_numpy(a).double() for a in (x, w, b))
+    ref = F.conv2d(xd, wd, bd, padding=ks // 2).clamp_min(0).numpy()
+    mag = F.conv2d(xd.abs(), wd.abs(), bd.abs(), padding=ks // 2).numpy()
+    e6 = np.abs(y6 - ref)
+    e32 = np.abs(y32 - ref)
+    assert (e6 <= 4e-6 * mag + 1e-6).all(), float((e6 / (4e-6 * mag + 1e-6)).max())
+    assert (e6 / np.maximum(mag, 1e-30)).mean() <= 3 * (e32 / np.maximum(mag, 1e-30)).mean() + 1e-9
+    assert np.array_equal(y6, y6x)  # split epilogue + rebuild is lossless
+
+
+def test_x6_split_roundtrip_exact(native, handle):
+    """A 1x1 identity conv through the X6 epilogue reproduces every fp32 input bit-exactly
+    (subnormal-free, both signs, magnitudes over 2^-60 .. 2^60)."""
+    rng = np.random.default_rng(3)
+    C, H, W = 16, 8, 8
+    mant = rng.uniform(1, 2, (1, C, H, W))
+    expo = rng.integers(-60, 60, (1, C, H, W))
+    sign = rng.choice([-1.0, 1.0], (1, C, H, W))
+    x = (sign * mant * np.exp2(expo)).astype(np.float32)
+    w = np.eye(C, dtype=np.float32).reshape(C, C, 1, 1)
+    b = np.zeros(C, np.float32)
+    y = _run(native, handle, native.lib.opose_debug_conv_x6, x, w, b, False, 64, 64, 0, 1)
+    assert np.array_equal(y, x)
+
+
+def test_network_x6_vs_f32_path(native):
+    """The default x6 network against the fp32 MFMA network (OPOSE_CONV=f32, read at handle
+    creation) on the same input: same maps within the network tolerance."""
+    from src import util
+    from src.model import bodypose_model
+    from src.weights import seeded_state_dict
+    sd = seeded_state_dict("body", 0)
+    x = np.random.default_rng(11).random((2, 3, 64, 96), dtype=np.float32) - np.float32(0.5)
+    m6 = bodypose_model(0)
+    m6.load_state_dict(util.transfer(m6, sd))
+    p6, h6 = m6(x)
+    old = os.environ.get("OPOSE_CONV")
+    os.environ["OPOSE_CONV"] = "f32"
+    try:
+        m32 = bodypose_model(0)
+    finally:
+        if old is None:
+            del os.environ["OPOSE_CONV"]
+        else:
+            os.environ["OPOSE_CONV"] = old
+    m32.load_state_dict(util.transfer(m32, sd))
+    p32, h32 = m32(x)
+    for a, r in ((p6, p32), (h6, h32)):
+        tol = 2e-4 * np.abs(r).max() + 2e-4 * np.abs(r)
+        assert (np.abs(a - r) <= tol).all()
