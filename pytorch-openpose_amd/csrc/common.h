@@ -77,6 +77,7 @@ struct X6Args {
     int nK;         // chunks of 32 k
     int Mpad, npix, ngroups, sk_grid;
     float* partial; // stream-K partial slabs [2 * sk_grid][MT * PT]
+    int ablate;     // timing ablations (0 in production): 1 no im2col DMA, 2 no weight DMA, 4 no barrier, 8 no LDS reads
 };
 
 // ---------------------------------------------------------------- body records

@@ -22,6 +22,7 @@
 //   fixup exactly as conv.hip.
 // * The epilogue adds bias, applies ReLU and writes the output split again (X6) into a
 //   group slice of a wider buffer (the CPM concat), or fp32 NCHW for the network outputs.
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <vector>
@@ -76,7 +77,7 @@ __device__ __forceinline__ void store4_x6(uint8_t* unit, uint32_t ps, const floa
 
 }  // namespace
 
-template <int MT, int PT, bool SMALL, int KS>
+template <int MT, int PT, bool SMALL, int KS, bool PIPE>
 __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int ks = KS ? KS : a.ks;
     const int taps = ks * ks;
@@ -160,107 +161,198 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             return ok ? pbase + (uint32_t)((dy * a.W + dx) * 16) : 0x80000000u;  // >= num_records -> 0
         };
         // im2col DMA of chunk c into stage buf: (piece, group) rows pg0, pg0 + WPJ, ...
-        auto dma_b = [&](int c, int buf) __attribute__((always_inline)) {
-            uint4* Bs = lds + buf * (A_U + B_U) + A_U;
-            uint32_t voff = 0;
-            int cb = 0;
+        // im2col DMA of chunk c, unit u of this wave ((piece, group) row pg0 + u * WPJ) into stage buf;
+        // voff / cb: the chunk's tap offset and channel block (b_prep)
+        struct BPrep {
+            uint32_t voff;
+            int cb;
+        };
+        auto b_prep = [&](int c) __attribute__((always_inline)) -> BPrep {
+            BPrep r{0u, 0};
             if constexpr (!SMALL) {
-                cb = c / taps;
-                voff = tap_off(c - cb * taps);
+                r.cb = c / taps;
+                r.voff = tap_off(c - r.cb * taps);
             }
+            return r;
+        };
+        auto dma_b_unit = [&](int c, const BPrep& bp, int buf, int u) __attribute__((always_inline)) {
+            uint4* Bs = lds + buf * (A_U + B_U) + A_U;
+            const int pg = pg0 + u * WPJ;
+            const int pc = pg >> 2, gi = pg & 3;
+            int grp;
+            uint32_t off;
+            if constexpr (SMALL) {
+                grp = 0;
+                off = tap_off(min(c * 4 + gi, taps - 1));  // padded taps: weights are 0
+            } else {
+                grp = min(bp.cb * 4 + gi, a.cin_g - 1);  // padded groups: any valid data (weights 0)
+                off = bp.voff;
+            }
+            const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(in_base + (size_t)pc * G.in_ps + (size_t)grp * HW * 16), (short)0, (int)0x80000000u,
+                0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + pg * PT + jw * 64), 16, off, 0, 0, 0);
+        };
+        auto dma_b = [&](int c, int buf) __attribute__((always_inline)) {
+            const BPrep bp = b_prep(c);
 #pragma unroll
-            for (int u = 0; u < B_PW; ++u) {
-                const int pg = pg0 + u * WPJ;
-                const int pc = pg >> 2, gi = pg & 3;
-                int grp;
-                uint32_t off;
-                if constexpr (SMALL) {
-                    grp = 0;
-                    off = tap_off(min(c * 4 + gi, taps - 1));  // padded taps: weights are 0
-                } else {
-                    grp = min(cb * 4 + gi, a.cin_g - 1);  // padded groups: any valid data (weights 0)
-                    off = voff;
-                }
-                const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-                    (void*)(in_base + (size_t)pc * G.in_ps + (size_t)grp * HW * 16), (short)0, (int)0x80000000u,
-                    0x00020000);
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + pg * PT + jw * 64), 16, off, 0, 0, 0);
-            }
+            for (int u = 0; u < B_PW; ++u) dma_b_unit(c, bp, buf, u);
+        };
+        auto dma_a_unit = [&](int c, int buf, int u) __attribute__((always_inline)) {
+            uint4* As = lds + buf * (A_U + B_U);
+            const int unit0 = (wave * A_PW + u) * 64;
+            const int pg = unit0 / MT, m = unit0 - pg * MT;
+            const uint8_t* src = G.wt + (((size_t)c * 12 + pg) * a.Mpad + m0 + m + lane) * 16;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + unit0), 16, 0, 0);
         };
         auto dma_a = [&](int c, int buf) __attribute__((always_inline)) {
-            uint4* As = lds + buf * (A_U + B_U);
 #pragma unroll
-            for (int u = 0; u < A_PW; ++u) {
-                const int unit0 = (wave * A_PW + u) * 64;
-                const int pg = unit0 / MT, m = unit0 - pg * MT;
-                const uint8_t* src = G.wt + (((size_t)c * 12 + pg) * a.Mpad + m0 + m + lane) * 16;
-                __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + unit0), 16, 0, 0);
-            }
+            for (int u = 0; u < A_PW; ++u) dma_a_unit(c, buf, u);
         };
 
-        dma_a(c_begin, 0);
-        dma_b(c_begin, 0);
-        __syncthreads();
-        for (int c = c_begin; c < c_end; ++c) {
-            const int buf = (c - c_begin) & 1;
-            const int cn = min(c + 1, c_end - 1);  // the last chunk re-loads itself into the free stage
-            const uint32_t a_lds =
-                (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + hk * MT + wm0 + l31);
-            const uint32_t b_lds =
-                (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + A_U + hk * PT + wp0 + l31);
-            i32x4 fa[2][3][TM], fb[2][3][TN];
-            auto read_step = [&](int s) __attribute__((always_inline)) {
+        i32x4 fa[2][3][TM], fb[2][3][TN];
+        auto lds_a = [&](int buf) __attribute__((always_inline)) {
+            return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + hk * MT + wm0 + l31);
+        };
+        auto lds_b = [&](int buf) __attribute__((always_inline)) {
+            return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + A_U + hk * PT + wp0 + l31);
+        };
+        // fragments of k-step s (16 k) of the stage at a_lds / b_lds
+        auto read_step = [&](int s, uint32_t a_lds, uint32_t b_lds) __attribute__((always_inline)) {
 #pragma unroll
-                for (int pc = 0; pc < 3; ++pc) {
+            for (int pc = 0; pc < 3; ++pc) {
 #pragma unroll
-                    for (int i = 0; i < TM; ++i)
-                        asm volatile("ds_read_b128 %0, %1 offset:%2"
-                                     : "=v"(fa[s][pc][i])
-                                     : "v"(a_lds), "i"(((pc * 4 + 2 * s) * MT + 32 * i) * 16));
+                for (int i = 0; i < TM; ++i)
+                    asm volatile("ds_read_b128 %0, %1 offset:%2"
+                                 : "=v"(fa[s][pc][i])
+                                 : "v"(a_lds), "i"(((pc * 4 + 2 * s) * MT + 32 * i) * 16));
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    asm volatile("ds_read_b128 %0, %1 offset:%2"
+                                 : "=v"(fb[s][pc][j])
+                                 : "v"(b_lds), "i"(((pc * 4 + 2 * s) * PT + 32 * j) * 16));
+            }
+        };
+        // the fragments of k-step s are in registers: make later uses depend on the wait
+        auto fence_step = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[s][pc][i]));
+#pragma unroll
+                for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(fb[s][pc][j]));
+            }
+        };
+        auto mfma_step = [&](int s) __attribute__((always_inline)) {
+            // small terms first: (2,0) (1,1) (0,2) (1,0) (0,1) (0,0)
+            constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
+            constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+            for (int t = 0; t < 6; ++t)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        asm volatile("ds_read_b128 %0, %1 offset:%2"
-                                     : "=v"(fb[s][pc][j])
-                                     : "v"(b_lds), "i"(((pc * 4 + 2 * s) * PT + 32 * j) * 16));
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                            __builtin_bit_cast(bf16x8, fa[s][PA[t]][i]), __builtin_bit_cast(bf16x8, fb[s][PB[t]][j]),
+                            acc[i][j], 0, 0, 0);
+        };
+
+        if constexpr (PIPE) {
+            // Software-pipelined chunk loop, one barrier per chunk, placed between the two k-steps:
+            //   step 0: 6*TM*TN MFMAs on the fragments of k-step 0, with the LDS reads of k-step 1
+            //           interleaved (one per MFMA gap);
+            //   wait for them, vmcnt(0) + barrier: every wave has read this stage, and the next
+            //           stage (its DMA issued one chunk earlier) has landed everywhere;
+            //   step 1: MFMAs of k-step 1, interleaved with the reads of the next chunk's k-step 0
+            //           and then the DMA of the chunk after it into this (now free) stage.
+            // sched_barrier pins the order: left alone the compiler sinks the MFMAs below the
+            // waits, exposing the LDS latency twice per chunk.
+            constexpr int NMF = 6 * TM * TN;   // MFMAs per k-step
+            constexpr int NRD = 3 * (TM + TN); // ds_read_b128 per k-step
+            constexpr int NDA = A_PW + B_PW;   // LDS-DMA instructions per chunk
+            constexpr int PA[6] = {2, 1, 0, 1, 0, 0};  // small terms first
+            constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
+            auto read_one = [&](int s, int r, uint32_t a_lds, uint32_t b_lds) __attribute__((always_inline)) {
+                const int pc = r / (TM + TN), k = r % (TM + TN);
+                if (k < TM)
+                    asm volatile("ds_read_b128 %0, %1 offset:%2"
+                                 : "=v"(fa[s][pc][k])
+                                 : "v"(a_lds), "i"(((pc * 4 + 2 * s) * MT + 32 * k) * 16));
+                else
+                    asm volatile("ds_read_b128 %0, %1 offset:%2"
+                                 : "=v"(fb[s][pc][k - TM])
+                                 : "v"(b_lds), "i"(((pc * 4 + 2 * s) * PT + 32 * (k - TM)) * 16));
+            };
+            auto mfma_one = [&](int s, int q) __attribute__((always_inline)) {
+                const int t = q / (TM * TN), i = (q / TN) % TM, j = q % TN;
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[s][PA[t]][i]),
+                                                                    __builtin_bit_cast(bf16x8, fb[s][PB[t]][j]),
+                                                                    acc[i][j], 0, 0, 0);
+            };
+            dma_a(c_begin, 0);
+            dma_b(c_begin, 0);
+            __syncthreads();
+            read_step(0, lds_a(0), lds_b(0));
+            {
+                const int cn = min(c_begin + 1, c_end - 1);
+                dma_a(cn, 1);
+                dma_b(cn, 1);
+            }
+            for (int c = c_begin; c < c_end; ++c) {
+                const int buf = (c - c_begin) & 1;
+                const uint32_t a_cur = lds_a(buf), b_cur = lds_b(buf);
+                const uint32_t a_nxt = lds_a(buf ^ 1), b_nxt = lds_b(buf ^ 1);
+                const int c2 = min(c + 2, c_end - 1);  // past the end: a harmless reload of the last chunk
+                const BPrep bp2 = b_prep(c2);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                fence_step(0);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < NMF; ++q) {
+                    mfma_one(0, q);
+#pragma unroll
+                    for (int r = q * NRD / NMF; r < (q + 1) * NRD / NMF; ++r) read_one(1, r, a_cur, b_cur);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
-            };
-            auto mfma_step = [&](int s) __attribute__((always_inline)) {
-                // small terms first: (2,0) (1,1) (0,2) (1,0) (0,1) (0,0)
-                constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
-                constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                fence_step(1);
+                __syncthreads();  // this stage read by all; next stage landed (vmcnt(0) first)
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int t = 0; t < 6; ++t)
+                for (int q = 0; q < NMF; ++q) {
+                    mfma_one(1, q);
 #pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                                __builtin_bit_cast(bf16x8, fa[s][PA[t]][i]), __builtin_bit_cast(bf16x8, fb[s][PB[t]][j]),
-                                acc[i][j], 0, 0, 0);
-            };
-            read_step(0);
-            dma_a(cn, buf ^ 1);
-            dma_b(cn, buf ^ 1);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[0][pc][i]));
-#pragma unroll
-                for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(fb[0][pc][j]));
+                    for (int o = q * (NRD + NDA) / NMF; o < (q + 1) * (NRD + NDA) / NMF; ++o) {
+                        if (o < NRD) read_one(0, o, a_nxt, b_nxt);
+                        else if (o < NRD + A_PW) dma_a_unit(c2, buf, o - NRD);
+                        else dma_b_unit(c2, bp2, buf, o - NRD - A_PW);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
-            read_step(1);
-            mfma_step(0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[1][pc][i]));
-#pragma unroll
-                for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(fb[1][pc][j]));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last (unused) reads landed
+            fence_step(0);
+        } else {
+            dma_a(c_begin, 0);
+            dma_b(c_begin, 0);
+            __syncthreads();
+            for (int c = c_begin; c < c_end; ++c) {
+                const int buf = (c - c_begin) & 1;
+                const int cn = min(c + 1, c_end - 1);  // the last chunk re-loads itself into the free stage
+                const int abl = a.ablate;              // timing ablations only (opose_debug_conv_x6_time)
+                if (!(abl & 8)) read_step(0, lds_a(buf), lds_b(buf));
+                if (!(abl & 2)) dma_a(cn, buf ^ 1);
+                if (!(abl & 1)) dma_b(cn, buf ^ 1);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                fence_step(0);
+                if (!(abl & 8)) read_step(1, lds_a(buf), lds_b(buf));
+                mfma_step(0);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                fence_step(1);
+                mfma_step(1);
+                if (!(abl & 4)) __syncthreads();  // next stage landed everywhere; this stage free
             }
-            mfma_step(1);
-            __syncthreads();  // next stage landed everywhere; this stage free
         }
 
         // ---- epilogue
@@ -532,19 +624,33 @@ void x6_pack_weights(const float* w, int cout, int cin, int ks, int Mpad, int* n
         }
 }
 
+static bool x6_pipe() {
+    static const bool on = [] {
+        const char* e = getenv("OPOSE_X6_PIPE");  // 0: the earlier two-wait chunk loop (A/B only)
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+template <int MT, int PT, bool PIPE>
+static void launch_x6_tile_p(const X6Args& a, hipStream_t st) {
+    const dim3 blk(64 * x6_waves(MT, PT));
+    if (a.small != 0)
+        hipLaunchKernelGGL((conv_x6<MT, PT, true, 0, PIPE>), dim3(a.sk_grid), blk, 0, st, a);
+    else if (a.ks == 7)
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 7, PIPE>), dim3(a.sk_grid), blk, 0, st, a);
+    else if (a.ks == 3)
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 3, PIPE>), dim3(a.sk_grid), blk, 0, st, a);
+    else if (a.ks == 1)
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 1, PIPE>), dim3(a.sk_grid), blk, 0, st, a);
+    else
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 0, PIPE>), dim3(a.sk_grid), blk, 0, st, a);
+}
+
 template <int MT, int PT>
 static void launch_x6_tile(const X6Args& a, hipStream_t st) {
-    const bool small = a.small != 0;
-    if (small)
-        hipLaunchKernelGGL((conv_x6<MT, PT, true, 0>), dim3(a.sk_grid), dim3(64 * x6_waves(MT, PT)), 0, st, a);
-    else if (a.ks == 7)
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 7>), dim3(a.sk_grid), dim3(64 * x6_waves(MT, PT)), 0, st, a);
-    else if (a.ks == 3)
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 3>), dim3(a.sk_grid), dim3(64 * x6_waves(MT, PT)), 0, st, a);
-    else if (a.ks == 1)
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 1>), dim3(a.sk_grid), dim3(64 * x6_waves(MT, PT)), 0, st, a);
-    else
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 0>), dim3(a.sk_grid), dim3(64 * x6_waves(MT, PT)), 0, st, a);
+    if (x6_pipe()) launch_x6_tile_p<MT, PT, true>(a, st);
+    else launch_x6_tile_p<MT, PT, false>(a, st);
     const int tiles = (a.Mpad / MT) * ((a.npix + PT - 1) / PT) * a.ngroups;
     if (a.sk_grid != tiles)
         hipLaunchKernelGGL((conv_x6_fixup<MT, PT>), dim3(tiles, MT * PT / 4 / 256), dim3(256), 0, st, a);

@@ -1799,6 +1799,7 @@ int opose_debug_conv_x6_time(opose_t* h, int N, int Cin, int H, int W, int Cout,
         a.ngroups = ngroups;
         a.sk_grid = t.grid;
         a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        if (const char* ab = getenv("OPOSE_X6_ABLATE")) a.ablate = atoi(ab);
         launch_conv_x6(a, t.mt, t.pt, h->stream);  // warm-up
         hipEvent_t e0, e1;
         OPOSE_HIP_CHECK(hipEventCreate(&e0));

@@ -1,0 +1,31 @@
+"""Times the split-bf16 conv kernel on the bench's layer shapes (32 frames of 184x328 input),
+default tile/stream-K choice; one JSON line per shape.  A/B: run under different OPOSE_X6_*
+environment settings."""
+import ctypes as C
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "pytorch-openpose_amd"))
+from src import _native  # noqa: E402
+
+h = _native.Handle(0)
+tag = os.environ.get("AB_TAG", "")
+ms = C.c_float()
+ablations = [int(v) for v in os.environ.get("AB_ABLATE", "0").split(",")]
+layers = os.environ.get("AB_LAYERS")
+for name, N, Cin, H, W, Cout, ks, ng in [("Mconv2-5", 32, 128, 23, 41, 128, 7, 2), ("Mconv1", 32, 185, 23, 41, 256, 7, 1),
+                                          ("conv1_2", 32, 64, 184, 328, 64, 3, 1),
+                                          ("conv2_2", 32, 128, 92, 164, 128, 3, 1),
+                                          ("conv3_x", 32, 256, 46, 82, 256, 3, 1),
+                                          ("conv4_2", 32, 512, 23, 41, 512, 3, 1),
+                                          ("stage1_3x3", 32, 128, 23, 41, 128, 3, 2)]:
+    if layers and name not in layers.split(","):
+        continue
+    flops = 2.0 * N * H * W * Cout * Cin * ks * ks * ng
+    for ab in ablations:  # OPOSE_X6_ABLATE bits (timing only, wrong results): see common.h X6Args
+        os.environ["OPOSE_X6_ABLATE"] = str(ab)
+        h.check(_native.lib.opose_debug_conv_x6_time(h.h, N, Cin, H, W, Cout, ks, ng, 0, 0, 0, 20, C.byref(ms)))
+        print(json.dumps(dict(tag=tag, layer=name, ablate=ab, ms=round(ms.value, 4),
+                              tf=round(flops / ms.value / 1e9, 1))), flush=True)
