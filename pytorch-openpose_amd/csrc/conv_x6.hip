@@ -24,6 +24,7 @@
 //   group slice of a wider buffer (the CPM concat), or fp32 NCHW for the network outputs.
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <stdexcept>
 #include <vector>
 
@@ -77,13 +78,19 @@ __device__ __forceinline__ void store4_x6(uint8_t* unit, uint32_t ps, const floa
 
 }  // namespace
 
-template <int MT, int PT, bool SMALL, int KS, bool PIPE>
+// MODE 0: two-wait chunk loop (A/B reference); 1: pipelined, v_mfma_f32_32x32x16_bf16;
+// 2: pipelined, v_mfma_f32_16x16x32_bf16 (one k-step per chunk)
+template <int MT, int PT, bool SMALL, int KS, int MODE>
 __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int ks = KS ? KS : a.ks;
     const int taps = ks * ks;
     constexpr int NW = x6_waves(MT, PT), NWM = NW == 8 ? MT / 64 : 2, NWP = NW / NWM;
     constexpr int WM = MT / NWM, WP = PT / NWP;
-    constexpr int TM = WM / 32, TN = WP / 32;
+    constexpr bool PIPE = MODE >= 1, S16 = MODE == 2;
+    constexpr int MB = S16 ? 16 : 32;            // MFMA block (rows = pixels)
+    constexpr int TM = WM / MB, TN = WP / MB;
+    constexpr int ACC_N = MB * MB / 64;          // accumulator registers per block
+    using AccT = typename std::conditional<S16, f32x4, floatx16>::type;
     constexpr int PJ = PT / 64;                  // 64-pixel runs per tile
     constexpr int A_U = 12 * MT, B_U = 12 * PT;  // 16-byte units per stage
     constexpr int A_PW = A_U / 64 / NW;          // A DMA instructions per wave per chunk
@@ -145,13 +152,13 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             pbase = (uint32_t)(n * G.in_cg * HW + r) * 16u;
         }
 
-        floatx16 acc[TM][TN];
+        AccT acc[TM][TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+                for (int r = 0; r < ACC_N; ++r) acc[i][j][r] = 0.f;
 
         auto tap_off = [&](int tap) __attribute__((always_inline)) -> uint32_t {
             const int ky = tap / ks;
@@ -210,7 +217,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             for (int u = 0; u < A_PW; ++u) dma_a_unit(c, buf, u);
         };
 
-        i32x4 fa[2][3][TM], fb[2][3][TN];
+        i32x4 fa[S16 ? 1 : 2][3][TM], fb[S16 ? 1 : 2][3][TN];
         auto lds_a = [&](int buf) __attribute__((always_inline)) {
             return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + hk * MT + wm0 + l31);
         };
@@ -252,13 +259,158 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                            __builtin_bit_cast(bf16x8, fa[s][PA[t]][i]), __builtin_bit_cast(bf16x8, fb[s][PB[t]][j]),
-                            acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < TN; ++j) {
+                        if constexpr (!S16)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                __builtin_bit_cast(bf16x8, fa[s][PA[t]][i]),
+                                __builtin_bit_cast(bf16x8, fb[s][PB[t]][j]), acc[i][j], 0, 0, 0);
+                    }
         };
 
-        if constexpr (PIPE) {
+        if constexpr (S16) {
+            // 16x16x32 MFMAs: a chunk (32 k) is one k-step.  Lane l holds row / pixel (l & 15) and
+            // the k-group (l >> 4) of its 16-row block; the LDS layout is the same [piece][group][row]
+            // unit array (ds_read_b128's 16-lane phases hit 4 rows of each of 4 groups: conflict free).
+            // One fragment set: the 6 piece products run as blocks of TM*TN MFMAs in the order
+            //   (0,2) (0,0) (0,1) | barrier | (1,0) (2,0) (1,1)
+            // and each piece's registers are refilled with the next chunk's fragments right after
+            // their last use in this chunk: R0 = A0, B2 (after block 2), R1 = B0, A2 (after block 4),
+            // R2 = B1, A1 (in the next chunk's block 0).  The barrier sits after block 2: by then
+            // every wave has read this chunk's stage (R2 waited before block 2) and the next stage
+            // has landed (vmcnt(0)), so the next chunk's R0 / R1 reads and the DMA of the chunk
+            // after it (into this stage) follow it, interleaved one per MFMA gap.
+            constexpr int PA[6] = {0, 0, 0, 1, 2, 1};
+            constexpr int PB[6] = {2, 0, 1, 0, 0, 1};
+            constexpr int NB = TM * TN;           // MFMAs per block
+            constexpr int TMN = TM + TN;          // reads per refill group
+            constexpr int NDA = A_PW + B_PW;      // LDS-DMA instructions per chunk
+            const int a16 = (lane >> 4) * MT + wm0 + (lane & 15);
+            const int b16 = (lane >> 4) * PT + wp0 + (lane & 15);
+            auto la = [&](int buf) __attribute__((always_inline)) {
+                return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + a16);
+            };
+            auto lb = [&](int buf) __attribute__((always_inline)) {
+                return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + A_U + b16);
+            };
+            // refill group g (0: A0 B2, 1: B0 A2, 2: B1 A1), read r of TMN
+            auto rd = [&](int g, int r, uint32_t abase, uint32_t bbase) __attribute__((always_inline)) {
+                const bool isA = g == 0 ? r < TM : r >= TN;
+                const int k = g == 0 ? (r < TM ? r : r - TM) : (r < TN ? r : r - TN);
+                const int pc = g == 0 ? (isA ? 0 : 2) : g == 1 ? (isA ? 2 : 0) : 1;
+                if (isA)
+                    asm volatile("ds_read_b128 %0, %1 offset:%2"
+                                 : "=v"(fa[0][pc][k])
+                                 : "v"(abase), "i"((pc * 4 * MT + 16 * k) * 16));
+                else
+                    asm volatile("ds_read_b128 %0, %1 offset:%2"
+                                 : "=v"(fb[0][pc][k])
+                                 : "v"(bbase), "i"((pc * 4 * PT + 16 * k) * 16));
+            };
+            auto mf = [&](int t, int q) __attribute__((always_inline)) {
+                const int i = q / TN, j = q % TN;
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[0][PA[t]][i]),
+                                                                    __builtin_bit_cast(bf16x8, fb[0][PB[t]][j]),
+                                                                    acc[i][j], 0, 0, 0);
+            };
+            auto fence_all = [&]() __attribute__((always_inline)) {
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[0][pc][i]));
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(fb[0][pc][j]));
+                }
+            };
+            dma_a(c_begin, 0);
+            dma_b(c_begin, 0);
+            __syncthreads();
+            {
+                const uint32_t a0 = la(0), b0 = lb(0);
+#pragma unroll
+                for (int r = 0; r < TMN; ++r) rd(0, r, a0, b0);
+#pragma unroll
+                for (int r = 0; r < TMN; ++r) rd(1, r, a0, b0);
+                const int cn = min(c_begin + 1, c_end - 1);
+                dma_a(cn, 1);
+                dma_b(cn, 1);
+            }
+            for (int c = c_begin; c < c_end; ++c) {
+                const int buf = (c - c_begin) & 1;
+                const uint32_t a_cur = la(buf), b_cur = lb(buf);
+                const uint32_t a_nxt = la(buf ^ 1), b_nxt = lb(buf ^ 1);
+                const int c2 = min(c + 2, c_end - 1);  // past the end: a harmless reload of the last chunk
+                const BPrep bp2 = b_prep(c2);
+                // block 0 (needs R0): R2 of this chunk interleaved
+                asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TMN > 15 ? 15 : TMN) : "memory");
+                fence_all();
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(0, q);
+#pragma unroll
+                    for (int r = q * TMN / NB; r < (q + 1) * TMN / NB; ++r) rd(2, r, a_cur, b_cur);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                // block 1 (needs R1)
+                asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TMN > 15 ? 15 : TMN) : "memory");
+                fence_all();
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(1, q);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                // block 2 (needs R2)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                fence_all();
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(2, q);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                __syncthreads();  // this stage read by all; the next stage landed (vmcnt(0) first)
+                __builtin_amdgcn_sched_barrier(0);
+                // blocks 3-5: R0 (block 3) and R1 (block 5) of the next chunk, DMA of chunk c2
+                constexpr int D3 = NDA / 3, D4 = 2 * NDA / 3;
+                auto dma_op = [&](int d) __attribute__((always_inline)) {
+                    if (d < A_PW) dma_a_unit(c2, buf, d);
+                    else dma_b_unit(c2, bp2, buf, d - A_PW);
+                };
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(3, q);
+                    constexpr int N3 = TMN + D3;
+#pragma unroll
+                    for (int o = q * N3 / NB; o < (q + 1) * N3 / NB; ++o) {
+                        if (o < TMN) rd(0, o, a_nxt, b_nxt);
+                        else dma_op(o - TMN);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(4, q);
+                    constexpr int N4 = D4 - D3;
+#pragma unroll
+                    for (int o = q * N4 / NB; o < (q + 1) * N4 / NB; ++o) dma_op(D3 + o);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(5, q);
+                    constexpr int N5 = TMN + NDA - D4;
+#pragma unroll
+                    for (int o = q * N5 / NB; o < (q + 1) * N5 / NB; ++o) {
+                        if (o < TMN) rd(1, o, a_nxt, b_nxt);
+                        else dma_op(D4 + o - TMN);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last (unused) reads landed
+            fence_all();
+        } else if constexpr (PIPE) {
             // Software-pipelined chunk loop, one barrier per chunk, placed between the two k-steps:
             //   step 0: 6*TM*TN MFMAs on the fragments of k-step 0, with the LDS reads of k-step 1
             //           interleaved (one per MFMA gap);
@@ -286,9 +438,10 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             };
             auto mfma_one = [&](int s, int q) __attribute__((always_inline)) {
                 const int t = q / (TM * TN), i = (q / TN) % TM, j = q % TN;
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[s][PA[t]][i]),
-                                                                    __builtin_bit_cast(bf16x8, fb[s][PB[t]][j]),
-                                                                    acc[i][j], 0, 0, 0);
+                if constexpr (!S16)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[s][PA[t]][i]),
+                                                                        __builtin_bit_cast(bf16x8, fb[s][PB[t]][j]),
+                                                                        acc[i][j], 0, 0, 0);
             };
             dma_a(c_begin, 0);
             dma_b(c_begin, 0);
@@ -356,19 +509,25 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         }
 
         // ---- epilogue
+        // accumulator register r of block (i, j): rows (channels) ml0 + (r & 3) of quad r >> 2,
+        // column (pixel) pl.  32x32: quad qd covers rows 32i + 8qd + 4hk .. +3, pixel 32j + l31;
+        // 16x16: rows 16i + 4(l >> 4) .. +3, pixel 16j + (l & 15).
         const bool whole = c_begin == 0 && c_end == nK;
         float* slab = a.partial + (size_t)(2 * id + (first ? 0 : 1)) * (MT * PT);
         const int cout8 = (G.cout + 7) & ~7;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const int pl = wp0 + j * 32 + l31;
+            const int pl = S16 ? wp0 + j * 16 + (lane & 15) : wp0 + j * 32 + l31;
             const int p = p0 + pl;
+            auto quad_row = [&](int i, int qd) __attribute__((always_inline)) {
+                return S16 ? wm0 + i * 16 + 4 * (lane >> 4) : wm0 + i * 32 + 8 * qd + 4 * hk;
+            };
             if (!whole) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int ml = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
+                    for (int r = 0; r < ACC_N; ++r) {
+                        const int ml = quad_row(i, r >> 2) + (r & 3);
                         asm volatile("global_store_dword %0, %1, off sc1" ::"v"(slab + ml * PT + pl),
                                      "v"(acc[i][j][r])
                                      : "memory");
@@ -381,29 +540,30 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int qd = 0; qd < 4; ++qd) {
-                    const int mg = m0 + wm0 + i * 32 + 8 * qd;  // first channel of the 8-group
+                for (int qd = 0; qd < ACC_N / 4; ++qd) {
+                    const int ml = quad_row(i, qd);  // first of 4 consecutive channels (half a group)
+                    const int mq = m0 + ml;
                     float v[4];
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
-                        v[t] = acc[i][j][4 * qd + t] + s_bias[mg - m0 + 4 * hk + t];
+                        v[t] = acc[i][j][4 * qd + t] + s_bias[ml + t];
                         if (G.relu) v[t] = fmaxf(v[t], 0.f);
                     }
                     if (G.out_f32) {
                         float* ob = static_cast<float*>(G.out) + ((size_t)n * G.out_c + G.out_off) * HW + rem;
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {
-                            const int m = mg + 4 * hk + t;
+                            const int m = mq + t;
                             if (m < G.cout) ob[(size_t)m * HW] = v[t];
                         }
-                    } else if (mg < cout8) {
-                        const int grp = mg >> 3;
+                    } else if (mq < cout8) {
+                        const int grp = mq >> 3, half = (mq >> 2) & 1;
                         store4_x6(static_cast<uint8_t*>(G.out) +
-                                      ((size_t)(n * G.out_c + G.out_off + grp) * HW + rem) * 16 + hk * 8,
+                                      ((size_t)(n * G.out_c + G.out_off + grp) * HW + rem) * 16 + half * 8,
                                   G.out_ps, v);
                         if (G.out2)
                             store4_x6(static_cast<uint8_t*>(G.out2) +
-                                          ((size_t)(n * G.out2_c + G.out2_off + grp) * HW + rem) * 16 + hk * 8,
+                                          ((size_t)(n * G.out2_c + G.out2_off + grp) * HW + rem) * 16 + half * 8,
                                       G.out2_ps, v);
                     }
                 }
@@ -624,33 +784,38 @@ void x6_pack_weights(const float* w, int cout, int cin, int ks, int Mpad, int* n
         }
 }
 
-static bool x6_pipe() {
-    static const bool on = [] {
-        const char* e = getenv("OPOSE_X6_PIPE");  // 0: the earlier two-wait chunk loop (A/B only)
-        return !(e && e[0] == '0');
+// main-loop variant: OPOSE_X6_MODE = 0 (two-wait loop), 1 (pipelined 32x32x16), 2 (pipelined
+// 16x16x32); default 2
+static int x6_mode() {
+    static const int m = [] {
+        const char* e = getenv("OPOSE_X6_MODE");
+        return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
     }();
-    return on;
+    return m;
 }
 
-template <int MT, int PT, bool PIPE>
-static void launch_x6_tile_p(const X6Args& a, hipStream_t st) {
+template <int MT, int PT, int MODE>
+static void launch_x6_tile_m(const X6Args& a, hipStream_t st) {
     const dim3 blk(64 * x6_waves(MT, PT));
     if (a.small != 0)
-        hipLaunchKernelGGL((conv_x6<MT, PT, true, 0, PIPE>), dim3(a.sk_grid), blk, 0, st, a);
+        hipLaunchKernelGGL((conv_x6<MT, PT, true, 0, MODE>), dim3(a.sk_grid), blk, 0, st, a);
     else if (a.ks == 7)
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 7, PIPE>), dim3(a.sk_grid), blk, 0, st, a);
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 7, MODE>), dim3(a.sk_grid), blk, 0, st, a);
     else if (a.ks == 3)
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 3, PIPE>), dim3(a.sk_grid), blk, 0, st, a);
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 3, MODE>), dim3(a.sk_grid), blk, 0, st, a);
     else if (a.ks == 1)
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 1, PIPE>), dim3(a.sk_grid), blk, 0, st, a);
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 1, MODE>), dim3(a.sk_grid), blk, 0, st, a);
     else
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 0, PIPE>), dim3(a.sk_grid), blk, 0, st, a);
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 0, MODE>), dim3(a.sk_grid), blk, 0, st, a);
 }
 
 template <int MT, int PT>
 static void launch_x6_tile(const X6Args& a, hipStream_t st) {
-    if (x6_pipe()) launch_x6_tile_p<MT, PT, true>(a, st);
-    else launch_x6_tile_p<MT, PT, false>(a, st);
+    switch (x6_mode()) {
+        case 0: launch_x6_tile_m<MT, PT, 0>(a, st); break;
+        case 1: launch_x6_tile_m<MT, PT, 1>(a, st); break;
+        default: launch_x6_tile_m<MT, PT, 2>(a, st); break;
+    }
     const int tiles = (a.Mpad / MT) * ((a.npix + PT - 1) / PT) * a.ngroups;
     if (a.sk_grid != tiles)
         hipLaunchKernelGGL((conv_x6_fixup<MT, PT>), dim3(tiles, MT * PT / 4 / 256), dim3(256), 0, st, a);
