@@ -66,10 +66,10 @@ def pmc_traffic():
         rec = json.load(open(path))
     except (OSError, ValueError):
         return None
-    # the 7x7 class runs one kernel instantiation (conv_x6<MT, PT, false, 7> /
+    # the 7x7 class runs one kernel instantiation (conv_x6<MT, PT, false, 7, MODE> /
     # conv_igemm_f32<MT, PT, true, 7, 0>); take the 7x7 instantiation with the most dispatches
     best = None
-    tag = ", false, 7>" if X6 else ", true, 7, 0>"
+    tag = ", false, 7," if X6 else ", true, 7, 0>"
     for name, v in rec.items():
         if CONV_KERNEL + "<" in name and tag in name and "hbm_bytes_per_launch" in v:
             if best is None or v.get("trace_calls", 0) > best.get("trace_calls", 0):

@@ -167,9 +167,10 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
             return ok ? pbase + (uint32_t)((dy * a.W + dx) * 16) : 0x80000000u;  // >= num_records -> 0
         };
-        // im2col DMA of chunk c into stage buf: (piece, group) rows pg0, pg0 + WPJ, ...
         // im2col DMA of chunk c, unit u of this wave ((piece, group) row pg0 + u * WPJ) into stage buf;
-        // voff / cb: the chunk's tap offset and channel block (b_prep)
+        // voff / cb: the chunk's tap offset and channel block (b_prep).  One buffer resource per
+        // piece plane; the group offset rides in soffset, the pixel + tap offset in voffset (the
+        // engine keeps a plane below 2^31 bytes, so 0x80000000 stays out of range either way)
         struct BPrep {
             uint32_t voff;
             int cb;
@@ -182,6 +183,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             }
             return r;
         };
+        const uint32_t grp_bytes = (uint32_t)HW * 16u;
         auto dma_b_unit = [&](int c, const BPrep& bp, int buf, int u) __attribute__((always_inline)) {
             uint4* Bs = lds + buf * (A_U + B_U) + A_U;
             const int pg = pg0 + u * WPJ;
@@ -196,21 +198,25 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
                 off = bp.voff;
             }
             const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(in_base + (size_t)pc * G.in_ps + (size_t)grp * HW * 16), (short)0, (int)0x80000000u,
-                0x00020000);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + pg * PT + jw * 64), 16, off, 0, 0, 0);
+                (void*)(in_base + (size_t)pc * G.in_ps), (short)0, (int)0x80000000u, 0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(Bs + pg * PT + jw * 64), 16, off,
+                                                     (int)((uint32_t)grp * grp_bytes), 0, 0);
         };
         auto dma_b = [&](int c, int buf) __attribute__((always_inline)) {
             const BPrep bp = b_prep(c);
 #pragma unroll
             for (int u = 0; u < B_PW; ++u) dma_b_unit(c, bp, buf, u);
         };
+        // weights: one buffer resource per chunk, the unit's row offset in soffset, lane * 16 in voffset
+        const uint32_t lane16 = (uint32_t)lane * 16u;
         auto dma_a_unit = [&](int c, int buf, int u) __attribute__((always_inline)) {
             uint4* As = lds + buf * (A_U + B_U);
             const int unit0 = (wave * A_PW + u) * 64;
             const int pg = unit0 / MT, m = unit0 - pg * MT;
-            const uint8_t* src = G.wt + (((size_t)c * 12 + pg) * a.Mpad + m0 + m + lane) * 16;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(As + unit0), 16, 0, 0);
+            const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(G.wt + (size_t)c * 12 * a.Mpad * 16), (short)0, (int)0x7fffffff, 0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(As + unit0), 16, lane16,
+                                                     (int)((uint32_t)(pg * a.Mpad + m0 + m) * 16u), 0, 0);
         };
         auto dma_a = [&](int c, int buf) __attribute__((always_inline)) {
 #pragma unroll
