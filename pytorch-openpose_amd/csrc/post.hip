@@ -57,16 +57,33 @@ struct GaussTile {
     double g[VR][GW];
 };
 
+__device__ __forceinline__ double gauss_skip_below(double thre) {
+    return thre > 0.0 ? thre * (1.0 - 1e-9) : -__builtin_inf();  // no skipping for thre <= 0
+}
+
+// Returns false (and leaves t unset) when every input pixel of the footprint is below
+// `skip_below`: the filter is a convex combination (weights > 0, sum 1), so no smoothed value of
+// the tile can then exceed the caller's threshold (skip_below = thre * (1 - 1e-9) covers the
+// float64 rounding of the 2 x 25-tap sums, < 1e-14 relative); NaN inputs count as below, as a
+// NaN in a pixel's support makes its comparison false in the reference too.
 template <typename T>
-__device__ __forceinline__ void gauss_tile(const T* __restrict__ m, int H, int W, int x0, int y0, GaussTile& t) {
+__device__ __forceinline__ bool gauss_tile(const T* __restrict__ m, int H, int W, int x0, int y0, GaussTile& t,
+                                           double skip_below) {
     const int tid = threadIdx.x;
-    if (tid < 2 * VW) {  // axis 0: thread -> (column c, half h)
-        const int c = tid % VW, h = tid / VW;
+    bool hot = false;
+    const bool vt = tid < 2 * VW;  // axis 0: thread -> (column c, half h)
+    const int c = tid % VW, h = tid / VW;
+    double win[VH + 24];
+    if (vt) {
         const T* col = m + reflect_idx(x0 - 13 + c, W);
         const int r0 = y0 - 13 + h * VH;  // image row of window entry 0
-        double win[VH + 24];
 #pragma unroll
         for (int i = 0; i < VH + 24; ++i) win[i] = (double)col[(size_t)reflect_idx(r0 + i, H) * W];
+#pragma unroll
+        for (int i = 0; i < VH + 24; ++i) hot |= win[i] >= skip_below;
+    }
+    if (!__syncthreads_or(hot)) return false;
+    if (vt) {
 #pragma unroll
         for (int i = 0; i < VH; ++i) {
             double acc = win[i + 12] * kGauss[0];
@@ -92,6 +109,7 @@ __device__ __forceinline__ void gauss_tile(const T* __restrict__ m, int H, int W
         }
     }
     __syncthreads();
+    return true;
 }
 
 // tile id -> (x tile, y tile, map) with an XCD-contiguous order (guide T1): horizontally and
@@ -117,7 +135,7 @@ __global__ __launch_bounds__(256) void gauss_nms(const T* __restrict__ avg, int 
     int x0, y0, np;
     gauss_tile_coords(H, W, x0, y0, np);
     const T* m = avg + (size_t)np * H * W;
-    gauss_tile(m, H, W, x0, y0, t);
+    if (!gauss_tile(m, H, W, x0, y0, t, gauss_skip_below(thre))) return;  // no pixel can pass `> thre`
     for (int e = threadIdx.x; e < TW * TH; e += 256) {
         const int r = e / TW, c = e - r * TW;
         const int y = y0 + r, x = x0 + c;
@@ -146,7 +164,14 @@ __global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict_
     int x0, y0, np;
     gauss_tile_coords(H, W, x0, y0, np);
     if (threadIdx.x == 0) s_n = 0;
-    gauss_tile(avg + (size_t)np * H * W, H, W, x0, y0, t);
+    if (!gauss_tile(avg + (size_t)np * H * W, H, W, x0, y0, t, gauss_skip_below(thre))) {
+        for (int e = threadIdx.x; e < TW * TH; e += 256) {  // nothing passes `> thre`
+            const int r = e / TW, c = e - r * TW;
+            const int y = y0 + r, x = x0 + c;
+            if (y < H && x < W) lab[(size_t)np * H * W + y * W + x] = -1;
+        }
+        return;
+    }
     int mine = 0;
     // a wave = one 64-pixel row segment of the tile: each set pixel points at the start of its
     // run inside the segment (union-find parent < itself), so cc_union only links runs

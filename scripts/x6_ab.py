@@ -24,8 +24,10 @@ for name, N, Cin, H, W, Cout, ks, ng in [("Mconv2-5", 32, 128, 23, 41, 128, 7, 2
     if layers and name not in layers.split(","):
         continue
     flops = 2.0 * N * H * W * Cout * Cin * ks * ks * ng
-    for ab in ablations:  # OPOSE_X6_ABLATE bits (timing only, wrong results): see common.h X6Args
+    for sp in [int(v) for v in os.environ.get("AB_SPLITS", "0").split(",")]:
+     for ab in ablations:  # OPOSE_X6_ABLATE bits (timing only, wrong results): see common.h X6Args
         os.environ["OPOSE_X6_ABLATE"] = str(ab)
-        h.check(_native.lib.opose_debug_conv_x6_time(h.h, N, Cin, H, W, Cout, ks, ng, 0, 0, 0, 20, C.byref(ms)))
-        print(json.dumps(dict(tag=tag, layer=name, ablate=ab, ms=round(ms.value, 4),
+        mt, pt = (128, 256) if sp else (0, 0)
+        h.check(_native.lib.opose_debug_conv_x6_time(h.h, N, Cin, H, W, Cout, ks, ng, mt, pt, sp, 20, C.byref(ms)))
+        print(json.dumps(dict(tag=tag + (f"sk{sp}" if sp else ""), layer=name, ablate=ab, ms=round(ms.value, 4),
                               tf=round(flops / ms.value / 1e9, 1))), flush=True)
