@@ -82,6 +82,14 @@ def pmc_traffic():
 # bytes the engine records per launch (csrc/engine.cpp prof_begin); the pair-scoring, matching
 # and assembly kernels are latency bound (a few hundred candidates per frame) -> no roofline.
 PEAK_HBM_GBS = 8000.0
+# gauss_nms is float64-VALU bound, not HBM bound: the reference's scipy filter is 2 separable
+# 25-tap passes per pixel, 37 float64 operations each (12 symmetric pair adds, 13 multiplies,
+# 12 accumulates; no FMA, scipy's order), on each of the 18 full-resolution part maps.  Peak:
+# MI355X float64 vector rate, 78.6 TFLOP/s counting an FMA as 2 -> 39.3 T non-FMA ops/s (AMD
+# spec figure; the tile skip of all-below-threshold footprints can make the algorithmic rate
+# exceed it on sparse maps).
+GAUSS_OPS_PER_PIXEL = 2 * 37
+PEAK_F64_OPS = 39.3e12
 LATENCY_STAGES = ("peaks_finalize", "paf_score", "limb_greedy", "assemble", "hand_cc")
 
 
@@ -94,6 +102,12 @@ def stage_roofline(prof):
             a = v["flops"] / (v["ms"] * 1e-3) / 1e12
             out[k] = {"bound": "mfma", "achieved": round(a, 2), "peak": round(PEAK_CONV_TFLOPS, 1),
                       "unit": "TFLOP/s", "frac": round(a / PEAK_CONV_TFLOPS, 4)}
+        elif k == "gauss_nms" and v.get("bytes", 0) > 0:
+            # bytes recorded per launch = 4 (f32 map) or 8 (f64 average) per map pixel
+            px = v["bytes"] / (4 if v.get("f32", True) else 8)
+            a = px * GAUSS_OPS_PER_PIXEL / (v["ms"] * 1e-3)
+            out[k] = {"bound": "valu_f64", "achieved": round(a / 1e12, 2), "peak": PEAK_F64_OPS / 1e12,
+                      "unit": "T float64 ops/s", "frac": round(a / PEAK_F64_OPS, 4)}
         elif k in LATENCY_STAGES or v.get("bytes", 0) <= 0:
             out[k] = {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None}
         else:

@@ -31,6 +31,13 @@
 #include "common.h"
 #include "kernels.h"
 
+// Compile-time timing ablations of the 16x16x32 main loop (0 in every shipped build; results
+// are wrong when set): 1 no im2col DMA, 2 no weight DMA, 8 no LDS fragment reads, 16 barrier
+// without the vmcnt(0) DMA wait, 32 no barrier.  Built by scripts/build_ablation.sh.
+#ifndef OPOSE_X6_ABL
+#define OPOSE_X6_ABL 0
+#endif
+
 namespace opose {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -300,6 +307,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             };
             // refill group g (0: A0 B2, 1: B0 A2, 2: B1 A1), read r of TMN
             auto rd = [&](int g, int r, uint32_t abase, uint32_t bbase) __attribute__((always_inline)) {
+                if constexpr ((OPOSE_X6_ABL & 8) != 0) return;
                 const bool isA = g == 0 ? r < TM : r >= TN;
                 const int k = g == 0 ? (r < TM ? r : r - TM) : (r < TN ? r : r - TN);
                 const int pc = g == 0 ? (isA ? 0 : 2) : g == 1 ? (isA ? 2 : 0) : 1;
@@ -375,13 +383,20 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
                     mf(2, q);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                __syncthreads();  // this stage read by all; the next stage landed (vmcnt(0) first)
+                if constexpr ((OPOSE_X6_ABL & 48) == 0) {
+                    __syncthreads();  // this stage read by all; the next stage landed (vmcnt(0) first)
+                } else if constexpr ((OPOSE_X6_ABL & 32) == 0) {
+                    __builtin_amdgcn_s_barrier();
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 // blocks 3-5: R0 (block 3) and R1 (block 5) of the next chunk, DMA of chunk c2
                 constexpr int D3 = NDA / 3, D4 = 2 * NDA / 3;
                 auto dma_op = [&](int d) __attribute__((always_inline)) {
-                    if (d < A_PW) dma_a_unit(c2, buf, d);
-                    else dma_b_unit(c2, bp2, buf, d - A_PW);
+                    if (d < A_PW) {
+                        if constexpr (!(OPOSE_X6_ABL & 2)) dma_a_unit(c2, buf, d);
+                    } else {
+                        if constexpr (!(OPOSE_X6_ABL & 1)) dma_b_unit(c2, bp2, buf, d - A_PW);
+                    }
                 };
 #pragma unroll
                 for (int q = 0; q < NB; ++q) {
