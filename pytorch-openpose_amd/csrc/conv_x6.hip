@@ -86,26 +86,28 @@ __device__ __forceinline__ void store4_x6(uint8_t* unit, uint32_t ps, const floa
 }  // namespace
 
 // MODE 0: two-wait chunk loop (A/B reference); 1: pipelined, v_mfma_f32_32x32x16_bf16;
-// 2: pipelined, v_mfma_f32_16x16x32_bf16 (one k-step per chunk)
+// 2: pipelined, v_mfma_f32_16x16x32_bf16 (one k-step per chunk); 3: as 2 with the im2col
+// fragments loaded straight from global memory into registers (LDS holds only the weights)
 template <int MT, int PT, bool SMALL, int KS, int MODE>
 __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int ks = KS ? KS : a.ks;
     const int taps = ks * ks;
     constexpr int NW = x6_waves(MT, PT), NWM = NW == 8 ? MT / 64 : 2, NWP = NW / NWM;
     constexpr int WM = MT / NWM, WP = PT / NWP;
-    constexpr bool PIPE = MODE >= 1, S16 = MODE == 2;
+    constexpr bool PIPE = MODE >= 1, S16 = MODE >= 2, BREG = MODE == 3;
     constexpr int MB = S16 ? 16 : 32;            // MFMA block (rows = pixels)
     constexpr int TM = WM / MB, TN = WP / MB;
     constexpr int ACC_N = MB * MB / 64;          // accumulator registers per block
     using AccT = typename std::conditional<S16, f32x4, floatx16>::type;
     constexpr int PJ = PT / 64;                  // 64-pixel runs per tile
-    constexpr int A_U = 12 * MT, B_U = 12 * PT;  // 16-byte units per stage
+    constexpr int A_U = 12 * MT, B_U = BREG ? 0 : 12 * PT;  // 16-byte units per stage (BREG: no B tile)
     constexpr int A_PW = A_U / 64 / NW;          // A DMA instructions per wave per chunk
     constexpr int WPJ = NW / PJ;                 // waves sharing one pixel run
     constexpr int B_PW = 12 / WPJ;               // B DMA instructions per wave per chunk
     static_assert(NW % PJ == 0 && 12 % WPJ == 0 && A_U % (64 * NW) == 0, "x6 tile");
 
-    __shared__ __attribute__((aligned(16))) uint4 lds[2 * (A_U + B_U)];
+    constexpr int STAGE_U = A_U + B_U;
+    __shared__ __attribute__((aligned(16))) uint4 lds[2 * STAGE_U];
     __shared__ float s_bias[MT];
 
     const int tid = threadIdx.x;
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         };
         const uint32_t grp_bytes = (uint32_t)HW * 16u;
         auto dma_b_unit = [&](int c, const BPrep& bp, int buf, int u) __attribute__((always_inline)) {
-            uint4* Bs = lds + buf * (A_U + B_U) + A_U;
+            uint4* Bs = lds + buf * STAGE_U + A_U;
             const int pg = pg0 + u * WPJ;
             const int pc = pg >> 2, gi = pg & 3;
             int grp;
@@ -217,7 +219,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         // weights: one buffer resource per chunk, the unit's row offset in soffset, lane * 16 in voffset
         const uint32_t lane16 = (uint32_t)lane * 16u;
         auto dma_a_unit = [&](int c, int buf, int u) __attribute__((always_inline)) {
-            uint4* As = lds + buf * (A_U + B_U);
+            uint4* As = lds + buf * STAGE_U;
             const int unit0 = (wave * A_PW + u) * 64;
             const int pg = unit0 / MT, m = unit0 - pg * MT;
             const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -232,10 +234,10 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
 
         i32x4 fa[S16 ? 1 : 2][3][TM], fb[S16 ? 1 : 2][3][TN];
         auto lds_a = [&](int buf) __attribute__((always_inline)) {
-            return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + hk * MT + wm0 + l31);
+            return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * STAGE_U + hk * MT + wm0 + l31);
         };
         auto lds_b = [&](int buf) __attribute__((always_inline)) {
-            return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + A_U + hk * PT + wp0 + l31);
+            return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * STAGE_U + A_U + hk * PT + wp0 + l31);
         };
         // fragments of k-step s (16 k) of the stage at a_lds / b_lds
         auto read_step = [&](int s, uint32_t a_lds, uint32_t b_lds) __attribute__((always_inline)) {
@@ -280,7 +282,182 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
                     }
         };
 
-        if constexpr (S16) {
+        if constexpr (BREG) {
+            // Weights through LDS (LDS-DMA, two stages, one barrier per chunk), im2col fragments
+            // straight from global memory into registers: lane l loads the 16-byte unit of pixel
+            // (l & 15) of each 16-pixel block, channel group (l >> 4) of the chunk, per piece --
+            // exactly its B fragment -- one chunk ahead into the other of two register sets.
+            // The two M-halves of the workgroup load the same units (L1 hits); LDS read bytes halve
+            // and the im2col LDS-DMA disappears.
+            constexpr int PA[6] = {0, 0, 0, 1, 2, 1};
+            constexpr int PB[6] = {2, 0, 1, 0, 0, 1};
+            constexpr int NB = TM * TN;
+            constexpr int NBL = 3 * TN;  // B loads per chunk
+            const int a16 = (lane >> 4) * MT + wm0 + (lane & 15);
+            auto la = [&](int buf) __attribute__((always_inline)) {
+                return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * STAGE_U + a16);
+            };
+            // A refill groups: 0 = A0 (after block 2), 1 = A2 (after block 4), 2 = A1 (next block 0)
+            auto rda = [&](int g, int k, uint32_t abase) __attribute__((always_inline)) {
+                const int pc = g == 0 ? 0 : g == 1 ? 2 : 1;
+                asm volatile("ds_read_b128 %0, %1 offset:%2"
+                             : "=v"(fa[0][pc][k])
+                             : "v"(abase), "i"((pc * 4 * MT + 16 * k) * 16));
+            };
+            // per-lane pixel of each block j: frame-relative row / column, byte offset of its unit
+            int by[TN], bx[TN];
+            uint32_t bbase[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int p = p0 + wp0 + 16 * j + (lane & 15);
+                const bool v = p < a.npix;
+                const int pc_ = v ? p : 0;
+                const int n = pc_ / HW;
+                const int r = pc_ - n * HW;
+                by[j] = v ? r / a.W : -100000;
+                bx[j] = r - (r / a.W) * a.W;
+                bbase[j] = (uint32_t)(n * G.in_cg * HW + r) * 16u;
+            }
+            const int gl = lane >> 4;
+            __amdgpu_buffer_rsrc_t brs[3];
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc)
+                brs[pc] = __builtin_amdgcn_make_buffer_rsrc((void*)(in_base + (size_t)pc * G.in_ps), (short)0,
+                                                             (int)0x80000000u, 0x00020000);
+            i32x4 fbr[2][3][TN];
+            // voffset of block j for chunk c (tap validity -> out-of-range marker), soffset = the
+            // chunk's channel-block offset
+            struct BOff {
+                uint32_t v[TN];
+                int s;
+            };
+            auto boff = [&](int c) __attribute__((always_inline)) -> BOff {
+                BOff o;
+                int tap, cb = 0, gi;
+                if constexpr (SMALL) {
+                    tap = min(c * 4 + gl, taps - 1);  // padded taps: weights are 0
+                    gi = 0;
+                } else {
+                    cb = c / taps;
+                    tap = c - cb * taps;
+                    gi = min(cb * 4 + gl, a.cin_g - 1) - cb * 4;  // padded groups: valid data, weights 0
+                }
+                const int ky = tap / ks;
+                const int dy = ky - a.pad, dx = tap - ky * ks - a.pad;
+                const uint32_t d = (uint32_t)((dy * a.W + dx) * 16) + (uint32_t)gi * grp_bytes;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const bool ok = (unsigned)(by[j] + dy) < (unsigned)a.H && (unsigned)(bx[j] + dx) < (unsigned)a.W;
+                    o.v[j] = ok ? bbase[j] + d : 0x80000000u;
+                }
+                o.s = (int)((uint32_t)(cb * 4) * grp_bytes);
+                return o;
+            };
+            auto ldb = [&](int set, int i, const BOff& o) __attribute__((always_inline)) {
+                const int pc = (i / TN + 2) % 3, j = i % TN;  // pieces in order of first use: 2, 0, 1
+                fbr[set][pc][j] = __builtin_amdgcn_raw_buffer_load_b128(brs[pc], o.v[j], o.s, 0);
+            };
+            auto fence_a = [&]() __attribute__((always_inline)) {
+#pragma unroll
+                for (int pc = 0; pc < 3; ++pc)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[0][pc][i]));
+            };
+            // one chunk with B register set SET: blocks 0-2, barrier, blocks 3-5
+            auto chunk = [&](int c, auto set_c) __attribute__((always_inline)) {
+                constexpr int SET = decltype(set_c)::value;
+                const int buf = (c - c_begin) & 1;
+                const uint32_t a_cur = la(buf), a_nxt = la(buf ^ 1);
+                const int c1 = min(c + 1, c_end - 1);  // past the end: harmless reloads
+                const int c2 = min(c + 2, c_end - 1);
+                const BOff ob = boff(c1);
+                auto mf = [&](int t, int q) __attribute__((always_inline)) {
+                    const int i = q / TN, j = q % TN;
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        __builtin_bit_cast(bf16x8, fa[0][PA[t]][i]), __builtin_bit_cast(bf16x8, fbr[SET][PB[t]][j]),
+                        acc[i][j], 0, 0, 0);
+                };
+                asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TM > 15 ? 15 : TM) : "memory");  // A0 (R0)
+                fence_a();
+                __builtin_amdgcn_sched_barrier(0);
+                // block 0: A1 refill of this chunk (R2) + the next chunk's B loads (first part)
+                constexpr int N0 = TM + NBL / 2;
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(0, q);
+#pragma unroll
+                    for (int o = q * N0 / NB; o < (q + 1) * N0 / NB; ++o) {
+                        if (o < TM) rda(2, o, a_cur);
+                        else ldb(SET ^ 1, o - TM, ob);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                constexpr int N1 = NBL - NBL / 2;
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(1, q);
+#pragma unroll
+                    for (int o = q * N1 / NB; o < (q + 1) * N1 / NB; ++o) ldb(SET ^ 1, NBL / 2 + o, ob);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(2, q);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                // this stage read by every wave (R2 waited); the next A stage landed: its DMA is
+                // older than the NBL B loads just issued
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(NBL) : "memory");
+                fence_a();
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                // blocks 3-5: A0 refill (R0) in block 3, A DMA of chunk c2 in block 4, A2 (R1) in 5
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(3, q);
+#pragma unroll
+                    for (int o = q * TM / NB; o < (q + 1) * TM / NB; ++o) rda(0, o, a_nxt);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(4, q);
+#pragma unroll
+                    for (int o = q * A_PW / NB; o < (q + 1) * A_PW / NB; ++o) dma_a_unit(c2, buf, o);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    mf(5, q);
+#pragma unroll
+                    for (int o = q * TM / NB; o < (q + 1) * TM / NB; ++o) rda(1, o, a_nxt);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            };
+            // prologue: A stage 0 landed, A0 / A2 fragments of the first chunk issued, its B loads
+            dma_a(c_begin, 0);
+            {
+                const BOff o0 = boff(c_begin);
+#pragma unroll
+                for (int i = 0; i < NBL; ++i) ldb(0, i, o0);
+            }
+            __syncthreads();
+            {
+                const uint32_t a0 = la(0);
+#pragma unroll
+                for (int k = 0; k < TM; ++k) rda(0, k, a0);
+#pragma unroll
+                for (int k = 0; k < TM; ++k) rda(1, k, a0);
+                dma_a(min(c_begin + 1, c_end - 1), 1);
+            }
+            for (int c = c_begin; c < c_end; c += 2) {
+                chunk(c, std::integral_constant<int, 0>());
+                if (c + 1 < c_end) chunk(c + 1, std::integral_constant<int, 1>());
+            }
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the last (unused) loads landed
+            fence_a();
+        } else if constexpr (S16) {
+
             // 16x16x32 MFMAs: a chunk (32 k) is one k-step.  Lane l holds row / pixel (l & 15) and
             // the k-group (l >> 4) of its 16-row block; the LDS layout is the same [piece][group][row]
             // unit array (ds_read_b128's 16-lane phases hit 4 rows of each of 4 groups: conflict free).
@@ -300,10 +477,10 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             const int a16 = (lane >> 4) * MT + wm0 + (lane & 15);
             const int b16 = (lane >> 4) * PT + wp0 + (lane & 15);
             auto la = [&](int buf) __attribute__((always_inline)) {
-                return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + a16);
+                return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * STAGE_U + a16);
             };
             auto lb = [&](int buf) __attribute__((always_inline)) {
-                return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * (A_U + B_U) + A_U + b16);
+                return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * STAGE_U + A_U + b16);
             };
             // refill group g (0: A0 B2, 1: B0 A2, 2: B1 A1), read r of TMN
             auto rd = [&](int g, int r, uint32_t abase, uint32_t bbase) __attribute__((always_inline)) {
@@ -810,7 +987,7 @@ void x6_pack_weights(const float* w, int cout, int cin, int ks, int Mpad, int* n
 static int x6_mode() {
     static const int m = [] {
         const char* e = getenv("OPOSE_X6_MODE");
-        return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
+        return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 2;
     }();
     return m;
 }
@@ -835,6 +1012,7 @@ static void launch_x6_tile(const X6Args& a, hipStream_t st) {
     switch (x6_mode()) {
         case 0: launch_x6_tile_m<MT, PT, 0>(a, st); break;
         case 1: launch_x6_tile_m<MT, PT, 1>(a, st); break;
+        case 3: launch_x6_tile_m<MT, PT, 3>(a, st); break;
         default: launch_x6_tile_m<MT, PT, 2>(a, st); break;
     }
     const int tiles = (a.Mpad / MT) * ((a.npix + PT - 1) / PT) * a.ngroups;

@@ -28,6 +28,8 @@ for name, N, Cin, H, W, Cout, ks, ng in [("Mconv2-5", 32, 128, 23, 41, 128, 7, 2
      for ab in ablations:  # OPOSE_X6_ABLATE bits (timing only, wrong results): see common.h X6Args
         os.environ["OPOSE_X6_ABLATE"] = str(ab)
         mt, pt = (128, 256) if sp else (0, 0)
+        if os.environ.get("AB_TILE"):  # e.g. AB_TILE=256x128
+            mt, pt = (int(v) for v in os.environ["AB_TILE"].split("x"))
         h.check(_native.lib.opose_debug_conv_x6_time(h.h, N, Cin, H, W, Cout, ks, ng, mt, pt, sp, 20, C.byref(ms)))
         print(json.dumps(dict(tag=tag + (f"sk{sp}" if sp else ""), layer=name, ablate=ab, ms=round(ms.value, 4),
                               tf=round(flops / ms.value / 1e9, 1))), flush=True)
