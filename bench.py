@@ -66,15 +66,16 @@ def pmc_traffic():
         rec = json.load(open(path))
     except (OSError, ValueError):
         return None
-    # the 7x7 class runs one kernel instantiation (conv_x6<MT, PT, false, 7, MODE> /
-    # conv_igemm_f32<MT, PT, true, 7, 0>); take the 7x7 instantiation with the most dispatches
-    best = None
+    # the 7x7 class runs as one or two kernel instantiations (conv_x6<MT, PT, false, 7, MODE>,
+    # 128x256 for the grouped 128-channel convs, 256x128 for Mconv1); dispatch-weighted mean
     tag = ", false, 7," if X6 else ", true, 7, 0>"
+    num = den = 0.0
     for name, v in rec.items():
         if CONV_KERNEL + "<" in name and tag in name and "hbm_bytes_per_launch" in v:
-            if best is None or v.get("trace_calls", 0) > best.get("trace_calls", 0):
-                best = v
-    return best["hbm_bytes_per_launch"] if best else None
+            w = v.get("trace_calls", 1) or 1
+            num += w * v["hbm_bytes_per_launch"]
+            den += w
+    return num / den if den else None
 
 
 # per-stage roofline (north_star: "achieved fraction of MFMA/HBM roofline reported per stage"):

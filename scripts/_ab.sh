@@ -1,12 +1,8 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONDONTWRITEBYTECODE=1
-rm -f gpurun_out/ab.log
-export AB_LAYERS=Mconv1,conv3_x,conv4_2
-for t in 128x256 256x128 128x256 256x128; do AB_TILE=$t AB_TAG=$t timeout -k 10 120 python scripts/x6_ab.py >> gpurun_out/ab.log 2>&1 || exit 1; done
-python - <<'PY'
-import json,collections
-d=collections.defaultdict(list)
-for l in open('gpurun_out/ab.log'):
-    if l.startswith('{'):
-        r=json.loads(l); d[r['layer']].append((r['tag'], r['tf']))
-for k,v in d.items(): print(f"{k:12s}", ' '.join(f'{t}:{x}' for t,x in v))
-PY
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_gpu_parity.py tests/test_gpu_hand.py > gpurun_out/pt.log 2>&1; rc=$?; tail -2 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
+for v in cur base cur base; do
+  if [ $v = cur ]; then L=pytorch-openpose_amd/lib/libopose.so; else L=alt_lib/$v.so; fi
+  OPOSE_LIB=$L timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu --latency-iters 0 > gpurun_out/b_$v.log 2>&1 || exit 1
+  python -c "
+import json; d=json.loads([l for l in open('gpurun_out/b_$v.log') if l.startswith('{')][-1]); s=d['stage_ms_per_step']; print('$v', round(d['value'],1), s['gauss_nms'], s['conv3x3'], s['conv7x7'])"
+done
