@@ -78,6 +78,7 @@ struct X6Args {
     int Mpad, npix, ngroups, sk_grid;
     float* partial; // stream-K partial slabs [2 * sk_grid][MT * PT]
     int ablate;     // timing ablations (0 in production): 1 no im2col DMA, 2 no weight DMA, 4 no barrier, 8 no LDS reads
+    int pool;       // 1: 2x2/2 max-pool fused into the epilogue (npix = N * (H/2) * (W/2) * 4, quad-major)
 };
 
 // ---------------------------------------------------------------- body records

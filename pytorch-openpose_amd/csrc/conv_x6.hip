@@ -117,6 +117,21 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
     const int nK = a.nK;
     const int HW = a.H * a.W;
+    // pooled conv (a.pool): GEMM columns run over the 2x2 quads of the pooled grid, quad-major
+    // (column q -> pooled pixel q >> 2, quadrant q & 3), so the epilogue pools 4 adjacent lanes
+    const int Wo = a.W >> 1, HWo = (a.H >> 1) * Wo;
+    auto decode = [&](int p, int& n, int& r) __attribute__((always_inline)) {  // column -> frame, y*W+x
+        if (a.pool) {
+            const int q = p >> 2, d = p & 3;
+            n = q / HWo;
+            const int ro = q - n * HWo;
+            const int yo = ro / Wo;
+            r = (2 * yo + (d >> 1)) * a.W + 2 * (ro - yo * Wo) + (d & 1);
+        } else {
+            n = p / HW;
+            r = p - n * HW;
+        }
+    };
     const int wm0 = (wave % NWM) * WM;
     const int wp0 = (wave / NWM) * WP;
     const int jw = wave % PJ;    // this wave's pixel run for the im2col DMA
@@ -153,9 +168,8 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         {
             const int p = p0 + jw * 64 + lane;
             const bool v = p < a.npix;
-            const int pc = v ? p : 0;
-            const int n = pc / HW;
-            const int r = pc - n * HW;
+            int n, r;
+            decode(v ? p : 0, n, r);
             py = v ? r / a.W : -100000;
             px = r - (r / a.W) * a.W;
             pbase = (uint32_t)(n * G.in_cg * HW + r) * 16u;
@@ -311,9 +325,8 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             for (int j = 0; j < TN; ++j) {
                 const int p = p0 + wp0 + 16 * j + (lane & 15);
                 const bool v = p < a.npix;
-                const int pc_ = v ? p : 0;
-                const int n = pc_ / HW;
-                const int r = pc_ - n * HW;
+                int n, r;
+                decode(v ? p : 0, n, r);
                 by[j] = v ? r / a.W : -100000;
                 bx[j] = r - (r / a.W) * a.W;
                 bbase[j] = (uint32_t)(n * G.in_cg * HW + r) * 16u;
@@ -729,6 +742,38 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
                         asm volatile("global_store_dword %0, %1, off sc1" ::"v"(slab + ml * PT + pl),
                                      "v"(acc[i][j][r])
                                      : "memory");
+                    }
+                continue;
+            }
+            if (a.pool) {
+                // 2x2 max over the quad's 4 lanes, then bias + ReLU (both monotone: identical to
+                // pooling the biased, rectified values), one lane per quad stores the pooled pixel.
+                // Whole tiles only (the host runs pooled convs data parallel), X6 output.
+                const int q = p >> 2;
+                const int n = q / HWo;
+                const int remo = q - n * HWo;
+                const bool lead = (lane & 3) == 0 && p < a.npix;
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int qd = 0; qd < ACC_N / 4; ++qd) {
+                        const int ml = quad_row(i, qd);
+                        const int mq = m0 + ml;
+                        float v[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            float m = acc[i][j][4 * qd + t];
+                            m = fmaxf(m, __shfl_xor(m, 1));
+                            m = fmaxf(m, __shfl_xor(m, 2));
+                            v[t] = m + s_bias[ml + t];
+                            if (G.relu) v[t] = fmaxf(v[t], 0.f);
+                        }
+                        if (lead && mq < cout8) {
+                            const int grp = mq >> 3, half = (mq >> 2) & 1;
+                            store4_x6(static_cast<uint8_t*>(G.out) +
+                                          ((size_t)(n * G.out_c + G.out_off + grp) * HWo + remo) * 16 + half * 8,
+                                      G.out_ps, v);
+                        }
                     }
                 continue;
             }

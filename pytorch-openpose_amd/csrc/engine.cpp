@@ -192,6 +192,12 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_CONV");
         return !(e && std::string(e) == "f32");
     }();
+    // MaxPool2d fused into the preceding conv's epilogue (default); OPOSE_FUSED_POOL=0 at handle
+    // creation: separate maxpool_x6 launches (A/B; bit-identical results)
+    bool fused_pool = [] {
+        const char* e = getenv("OPOSE_FUSED_POOL");
+        return !(e && e[0] == '0');
+    }();
     DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[kMaxScales], avg, cnt, list, peak_pos, part_cnt,
         score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score, skcnt, hsel;
     // stream-K: split tiles reduced by the conv_sk_fixup launch (default) or in-kernel by the
@@ -529,8 +535,10 @@ static XAct x6act(uint8_t* p, int cg, int goff, size_t npix) {
     return XAct{p, cg, goff, (uint32_t)ps, false};
 }
 
+// pool: MaxPool2d(2, 2) (src/model.py:10-13, floor mode) fused into the epilogue; out0 is then the
+// pooled [N][(H/2)(W/2)] X6 tensor (conv outputs the floor mode drops are never computed)
 static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W, XAct in0, XAct out0, XAct in1,
-                        XAct out1, bool relu0, bool relu1, XAct dup = XAct{}) {
+                        XAct out1, bool relu0, bool relu1, XAct dup = XAct{}, bool pool = false) {
     X6Args a{};
     const int ng = c1 ? 2 : 1;
     a.N = N;
@@ -542,7 +550,9 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
     a.small = c0->small6 ? 1 : 0;
     a.nK = c0->nK6;
     a.Mpad = c0->Mpad;
-    a.npix = N * H * W;
+    a.npix = pool ? N * (H / 2) * (W / 2) * 4 : N * H * W;
+    a.pool = pool ? 1 : 0;
+    if (pool && (c1 || dup.p || out0.f32)) throw std::invalid_argument("pooled conv: single X6 output only");
     DevConv* cs[2] = {c0, c1};
     XAct ins[2] = {in0, in1}, outs[2] = {out0, out1};
     bool relus[2] = {relu0, relu1};
@@ -570,7 +580,8 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
         a.g[0].out2_off = dup.off;
     }
     if (ng == 1) a.g[1] = a.g[0];
-    const TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.nK, true);
+    TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.nK, true);
+    if (pool) t.grid = (a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * ng;  // whole tiles (data parallel)
     a.ngroups = ng;
     a.sk_grid = t.grid;
     a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
@@ -608,12 +619,23 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
         uint8_t* dst = (cur == A) ? B : A;
         const int og = (s.cout + 7) / 8;
         const size_t np = (size_t)N * hh * ww;
+        const bool pooled = s.name == "conv1_2" || s.name == "conv2_2" || s.name == "conv3_4";
+        if (pooled && h->fused_pool) {  // conv + MaxPool2d(2, 2) in one launch
+            run_conv_x6(h, c, nullptr, N, hh, ww, x6act(cur, cg, 0, np),
+                        x6act(dst, og, 0, (size_t)N * (hh / 2) * (ww / 2)), XAct{}, XAct{}, true, false, XAct{},
+                        true);
+            cur = dst;
+            cg = og;
+            hh /= 2;
+            ww /= 2;
+            continue;
+        }
         XAct out = final_layer ? last : x6act(dst, og, 0, np);
         run_conv_x6(h, c, nullptr, N, hh, ww, x6act(cur, cg, 0, np), out, XAct{}, XAct{}, true, false,
                     final_layer ? dup : XAct{});
         cur = dst;
         cg = og;
-        if (s.name == "conv1_2" || s.name == "conv2_2" || s.name == "conv3_4") {
+        if (pooled) {
             uint8_t* pd = (cur == A) ? B : A;
             ProfEntry pe;
             h->prof_begin(pe, "maxpool", 0, (double)np * cg * 48 * 1.25);

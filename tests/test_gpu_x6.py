@@ -112,3 +112,36 @@ def test_network_x6_vs_f32_path(native):
     for a, r in ((p6, p32), (h6, h32)):
         tol = 2e-4 * np.abs(r).max() + 2e-4 * np.abs(r)
         assert (np.abs(a - r) <= tol).all()
+
+
+def test_network_fused_pool(native):
+    """MaxPool2d fused into the conv epilogue (default) against separate maxpool launches
+    (OPOSE_FUSED_POOL=0, read at handle creation): max then bias + ReLU is the same value as
+    bias + ReLU then max, so a pooled layer's output equals pool(conv) exactly when the conv sums
+    in the same order; the fused launch always runs whole tiles while the separate conv may be
+    split over the k range (stream-K) at these small sizes, so the bar is fp32 summation-order
+    noise: the network tolerance, and a maximum deviation below 1e-5 of the map's range."""
+    from src import util
+    from src.model import bodypose_model, handpose_model
+    from src.weights import seeded_state_dict
+    for kind, cls, shape in (("body", bodypose_model, (2, 3, 72, 104)), ("hand", handpose_model, (1, 3, 88, 88))):
+        sd = seeded_state_dict(kind, 0)
+        x = np.random.default_rng(5).random(shape, dtype=np.float32) - np.float32(0.5)
+        outs = []
+        for fused in ("1", "0"):
+            old = os.environ.get("OPOSE_FUSED_POOL")
+            os.environ["OPOSE_FUSED_POOL"] = fused
+            try:
+                m = cls(0)
+            finally:
+                if old is None:
+                    del os.environ["OPOSE_FUSED_POOL"]
+                else:
+                    os.environ["OPOSE_FUSED_POOL"] = old
+            m.load_state_dict(util.transfer(m, sd))
+            y = m(x)
+            outs.append(y if isinstance(y, tuple) else (y,))
+        for a, r in zip(*outs):
+            tol = 2e-4 * np.abs(r).max() + 2e-4 * np.abs(r)
+            assert (np.abs(a - r) <= tol).all(), kind
+            assert np.abs(a - r).max() <= 1e-5 * np.abs(r).max(), kind
