@@ -1092,6 +1092,75 @@ void launch_from_x6(const uint8_t* in, int cg, int goff, uint32_t ps, int C, int
                        goff, ps, C, N, HW, out, cstride, coff);
 }
 
+// The first conv (conv1_1: Cin = 3, 3x3, 64 outputs, ReLU; src/model.py:37 / :141) directly on
+// the fp32 network input: one thread per output pixel holds its 27 inputs and produces all 64
+// channels with fp32 FMAs (packed pairs), weights read as uniform scalars, X6 output.  The
+// implicit GEMM would pad K = 27 to 3 chunks of 32 and spend the launch on tile prologues; this
+// kernel is bound by its 384-byte-per-pixel X6 store.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <int CIN>
+__global__ __launch_bounds__(256) void conv_first_x6_kernel(const float* __restrict__ x, int N, int H, int W,
+                                                            const float* __restrict__ wt, int Mpad,
+                                                            const float* __restrict__ bias, uint8_t* __restrict__ out,
+                                                            uint32_t ops) {
+    const int HW = H * W;
+    const size_t total = (size_t)N * HW;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int n = (int)(e / HW);
+        const int r = (int)(e - (size_t)n * HW);
+        const int y = r / W, xx = r - (r / W) * W;
+        float in[CIN * 9];
+#pragma unroll
+        for (int c = 0; c < CIN; ++c)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int iy = y + t / 3 - 1, ix = xx + t % 3 - 1;
+                const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+                in[c * 9 + t] = ok ? x[((size_t)n * CIN + c) * HW + iy * W + ix] : 0.f;
+            }
+        uint8_t* o = out + ((size_t)n * 8 * HW + r) * 16;
+#pragma unroll 1
+        for (int g = 0; g < 8; ++g) {
+            f32x2 acc[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+            for (int k = 0; k < CIN * 9; ++k) {
+                const f32x2 xv = {in[k], in[k]};
+                const float* wk = wt + (size_t)k * Mpad + g * 8;  // K order = (channel, tap): OIHW
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const f32x2 wv = {wk[2 * q], wk[2 * q + 1]};
+                    acc[q] = __builtin_elementwise_fma(xv, wv, acc[q]);
+                }
+            }
+            float v[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                v[2 * q] = fmaxf(acc[q].x + bias[g * 8 + 2 * q], 0.f);
+                v[2 * q + 1] = fmaxf(acc[q].y + bias[g * 8 + 2 * q + 1], 0.f);
+            }
+            uint32_t hp[3][8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) split3(v[k], hp[0][k], hp[1][k], hp[2][k]);
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) {
+                uint4 w4;
+                w4.x = hp[pc][0] | (hp[pc][1] << 16);
+                w4.y = hp[pc][2] | (hp[pc][3] << 16);
+                w4.z = hp[pc][4] | (hp[pc][5] << 16);
+                w4.w = hp[pc][6] | (hp[pc][7] << 16);
+                *reinterpret_cast<uint4*>(o + (size_t)g * HW * 16 + (size_t)pc * ops) = w4;
+            }
+        }
+    }
+}
+
+void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const float* wt, int Mpad, const float* bias,
+                          uint8_t* out, uint32_t ops, hipStream_t st) {
+    if (Cin != 3) throw std::invalid_argument("conv_first_x6: Cin must be 3");
+    const int grid = grid_for((size_t)N * H * W);
+    hipLaunchKernelGGL(conv_first_x6_kernel<3>, dim3(grid), dim3(256), 0, st, x, N, H, W, wt, Mpad, bias, out, ops);
+}
+
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,
                        hipStream_t st) {
     hipLaunchKernelGGL(maxpool_x6_kernel, dim3(grid_for((size_t)NG * (H / 2) * (W / 2))), dim3(256), 0, st, in, ips,

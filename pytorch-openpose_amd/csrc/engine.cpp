@@ -198,6 +198,11 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_FUSED_POOL");
         return !(e && e[0] == '0');
     }();
+    // conv1_1 by the direct first-layer kernel (default); OPOSE_FIRST_DIRECT=0: implicit GEMM
+    bool first_direct = [] {
+        const char* e = getenv("OPOSE_FIRST_DIRECT");
+        return !(e && e[0] == '0');
+    }();
     DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[kMaxScales], avg, cnt, list, peak_pos, part_cnt,
         score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score, skcnt, hsel;
     // stream-K: split tiles reduced by the conv_sk_fixup launch (default) or in-kernel by the
@@ -600,21 +605,33 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
 static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, int W, XAct last, XAct dup) {
     const std::vector<Spec> vgg = net == OPOSE_NET_BODY ? vgg_body() : vgg_hand();
     const size_t npix = (size_t)N * H * W;
-    uint8_t* X = h->x6in.ensure<uint8_t>(npix * 16 * 3, h->stream);
-    {
-        ProfEntry pe;
-        h->prof_begin(pe, "to_x6", 0, (double)npix * (12 + 48));
-        launch_to_x6(x, 3, 0, 3, N, H * W, X, 1, 0, (uint32_t)(npix * 16), h->stream);
-        h->prof_end(pe);
-    }
     const size_t act = npix * 8 * 16 * 3;  // 64 channels at full resolution = the largest trunk tensor
     uint8_t* A = h->x6A.ensure<uint8_t>(act, h->stream);
     uint8_t* B = h->x6B.ensure<uint8_t>(act, h->stream);
-    uint8_t* cur = X;
+    uint8_t* cur = nullptr;
     int cg = 1, hh = H, ww = W;
     for (size_t i = 0; i < vgg.size(); ++i) {
         const Spec& s = vgg[i];
         DevConv* c = find_conv(h, net, s.name);
+        if (i == 0 && s.cin == 3 && s.cout == 64 && s.ks == 3 && s.pad == 1 && vgg.size() > 1 && h->first_direct) {
+            // conv1_1 straight from the fp32 input (conv_first_x6), no input split
+            ProfEntry pe;
+            h->prof_begin(pe, "conv3x3", 2.0 * 64 * 27 * (double)npix, 0);
+            if (h->detail) pe.detail = "layer/" + s.name + "/first_direct/n" + std::to_string(npix);
+            launch_conv_first_x6(x, N, 3, H, W, c->wt, c->Mpad, c->bias, A, (uint32_t)(npix * 8 * 16), h->stream);
+            h->prof_end(pe);
+            cur = A;
+            cg = 8;
+            continue;
+        }
+        if (i == 0) {
+            uint8_t* X = h->x6in.ensure<uint8_t>(npix * 16 * 3, h->stream);
+            ProfEntry pe;
+            h->prof_begin(pe, "to_x6", 0, (double)npix * (12 + 48));
+            launch_to_x6(x, 3, 0, 3, N, H * W, X, 1, 0, (uint32_t)(npix * 16), h->stream);
+            h->prof_end(pe);
+            cur = X;
+        }
         const bool final_layer = i + 1 == vgg.size();
         uint8_t* dst = (cur == A) ? B : A;
         const int og = (s.cout + 7) / 8;

@@ -38,6 +38,8 @@ void launch_to_x6(const float* in, int cstride, int coff, int C, int N, int HW, 
                   uint32_t ps, hipStream_t st);
 void launch_from_x6(const uint8_t* in, int cg, int goff, uint32_t ps, int C, int N, int HW, float* out, int cstride,
                     int coff, hipStream_t st);
+void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const float* wt, int Mpad, const float* bias,
+                          uint8_t* out, uint32_t ops, hipStream_t st);
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,
                        hipStream_t st);
 

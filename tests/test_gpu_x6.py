@@ -114,13 +114,15 @@ def test_network_x6_vs_f32_path(native):
         assert (np.abs(a - r) <= tol).all()
 
 
-def test_network_fused_pool(native):
-    """MaxPool2d fused into the conv epilogue (default) against separate maxpool launches
-    (OPOSE_FUSED_POOL=0, read at handle creation): max then bias + ReLU is the same value as
-    bias + ReLU then max, so a pooled layer's output equals pool(conv) exactly when the conv sums
-    in the same order; the fused launch always runs whole tiles while the separate conv may be
-    split over the k range (stream-K) at these small sizes, so the bar is fp32 summation-order
-    noise: the network tolerance, and a maximum deviation below 1e-5 of the map's range."""
+@pytest.mark.parametrize("env", ["OPOSE_FUSED_POOL", "OPOSE_FIRST_DIRECT"])
+def test_network_variants(native, env):
+    """Default network against the variant with one optimisation switched off (read at handle
+    creation): OPOSE_FUSED_POOL=0 runs MaxPool2d as separate launches instead of in the conv
+    epilogue (max then bias + ReLU is the same value as bias + ReLU then max: equal whenever the
+    conv sums in the same order; the fused launch always runs whole tiles while the separate conv
+    may be split over k at these small sizes); OPOSE_FIRST_DIRECT=0 runs conv1_1 as an implicit
+    GEMM instead of the direct fp32-FMA kernel.  Bar: fp32 summation-order noise -- the network
+    tolerance, and a maximum deviation below 1e-5 of the map's range."""
     from src import util
     from src.model import bodypose_model, handpose_model
     from src.weights import seeded_state_dict
@@ -128,16 +130,16 @@ def test_network_fused_pool(native):
         sd = seeded_state_dict(kind, 0)
         x = np.random.default_rng(5).random(shape, dtype=np.float32) - np.float32(0.5)
         outs = []
-        for fused in ("1", "0"):
-            old = os.environ.get("OPOSE_FUSED_POOL")
-            os.environ["OPOSE_FUSED_POOL"] = fused
+        for on in ("1", "0"):
+            old = os.environ.get(env)
+            os.environ[env] = on
             try:
                 m = cls(0)
             finally:
                 if old is None:
-                    del os.environ["OPOSE_FUSED_POOL"]
+                    del os.environ[env]
                 else:
-                    os.environ["OPOSE_FUSED_POOL"] = old
+                    os.environ[env] = old
             m.load_state_dict(util.transfer(m, sd))
             y = m(x)
             outs.append(y if isinstance(y, tuple) else (y,))
