@@ -58,6 +58,11 @@ def parse():
     return ap.parse_args()
 
 
+# frames are resident and static for the whole run, so every step may overlap its network with
+# the previous step's post-processing (OPOSE_PIPELINE; BENCH_PIPELINE=0 for the serial A/B)
+PIPELINE = os.environ.get("BENCH_PIPELINE", "1") != "0"
+
+
 def pmc_traffic():
     """HBM bytes per 7x7-conv launch from the committed rocprofv3 PMC summary (separate
     --pmc passes of this same bench; scripts/gpu_profile.sh + scripts/pmc_summary.py)."""
@@ -170,7 +175,7 @@ def main():
     from src.dist import gather_records
 
     def step():
-        body.infer_records(frames, rec)
+        body.infer_records(frames, rec, pipeline=PIPELINE)
         if world > 1:
             # RCCL all_gather of the per-frame keypoint records, ordered after the library's
             # kernels on its stream (src/dist.py)
@@ -247,7 +252,9 @@ def main():
             "config": {"workload": f"C2/C4: Body() on 368x656 frames, {B} frames per GPU per step, "
                                    f"RCCL all_gather of per-frame keypoint records when n_gpus > 1",
                        "frame": [H, W], "frames_per_gpu_per_step": B, "scale_search": [0.5],
-                       "net_input": [184, 328], "parallelism": f"frame-sharded dp{world}"},
+                       "net_input": [184, 328], "parallelism": f"frame-sharded dp{world}",
+                       "step_overlap": "network of step k+1 overlaps post-processing of step k (OPOSE_PIPELINE)"
+                       if PIPELINE else "none"},
             "roofline": {"bound": "mfma", "kernel": CONV_KERNEL + " (7x7 CPM stages)",
                          "achieved": achieved, "peak": PEAK_CONV_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_CONV_TFLOPS,

@@ -52,6 +52,14 @@ enum {
     OPOSE_IN_DEVICE = 1,     /* input pointer is device memory                      */
     OPOSE_OUT_DEVICE = 2,    /* output pointer is device memory; call is async on the
                                 handle's stream                                     */
+    OPOSE_PIPELINE = 4,      /* opose_body_infer with IN_DEVICE | OUT_DEVICE only: the
+                                input frames are complete when the call is made (not
+                                produced by work still queued on the handle's stream) and
+                                stay unmodified until the handle's stream passes the
+                                call. The call's network part then runs on a second
+                                stream and overlaps the previous call's post-network
+                                part; records are still complete in the handle's stream
+                                order. Video-batch throughput mode.                 */
 };
 
 #define OPOSE_MAX_SCALES 8

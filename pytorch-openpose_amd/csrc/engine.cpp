@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -108,7 +109,8 @@ struct DevBuf {
         size_t b = n * sizeof(T);
         if (b > bytes) {
             if (p) {
-                OPOSE_HIP_CHECK(hipStreamSynchronize(st));
+                (void)st;
+                OPOSE_HIP_CHECK(hipDeviceSynchronize());  // the handle may have work on two streams
                 OPOSE_HIP_CHECK(hipFree(p));
                 p = nullptr;
             }
@@ -203,8 +205,27 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_FIRST_DIRECT");
         return !(e && e[0] == '0');
     }();
-    DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[kMaxScales], avg, cnt, list, peak_pos, part_cnt,
-        score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score, skcnt, hsel;
+    DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[2][kMaxScales], avg, cnt, list, peak_pos,
+        part_cnt, score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score, skcnt, hsel;
+    // Cross-call pipelining of opose_body_infer calls flagged OPOSE_PIPELINE (device input and
+    // output; OPOSE_PIPELINE=0 in the environment at handle creation: never).  Call k's network part (preprocess, conv stack,
+    // x8 upsample) runs on `nstream`, its post-network part on `stream` after an event; call
+    // k+1's network then overlaps call k's post-network kernels (latency-bound launches of a few
+    // dozen workgroups, and the CUs a 236-tile conv grid leaves idle).  The x8 maps (the only
+    // buffers both parts touch) alternate between two sets; `nstream` waits for the post part
+    // of the call two back before overwriting a set, and for `stream` whenever another entry
+    // point used the shared network workspace there since (main_dirty).  Every call ends with
+    // `stream` ordered after its own network part.
+    bool pipeline = [] {
+        const char* e = getenv("OPOSE_PIPELINE");
+        return !(e && e[0] == '0');
+    }();
+    hipStream_t nstream = nullptr;
+    hipEvent_t ev_net = nullptr, ev_main = nullptr, ev_post[2] = {nullptr, nullptr};
+    bool post_pending[2] = {false, false};
+    bool main_dirty = false;
+    int mid_set = 0, next_set = 0;
+    DevBuf& mid(int s) { return mids[mid_set][s]; }
     // stream-K: split tiles reduced by the conv_sk_fixup launch (default) or in-kernel by the
     // last arriving workgroup (OPOSE_SK_INKERNEL=1; measured 0.4 % slower at batch 32: the
     // reducing workgroup's serial slab reads stall its next tile more than the launch costs)
@@ -249,8 +270,13 @@ struct opose_ctx {
         OPOSE_HIP_CHECK(hipEventRecord(pe.e1, stream));
         pending.push_back(pe);
     }
-    void prof_drain() {
+    // fold finished event pairs into agg; non-blocking (stops at the first unfinished pair, so a
+    // call does not wait for its own kernels) unless `all`
+    void prof_drain(bool all = false) {
+        size_t done = 0;
         for (auto& pe : pending) {
+            if (!all && hipEventQuery(pe.e1) != hipSuccess) break;
+            ++done;
             OPOSE_HIP_CHECK(hipEventSynchronize(pe.e1));
             float ms = 0;
             OPOSE_HIP_CHECK(hipEventElapsedTime(&ms, pe.e0, pe.e1));
@@ -265,9 +291,15 @@ struct opose_ctx {
             event_pool.push_back(pe.e0);
             event_pool.push_back(pe.e1);
         }
-        pending.clear();
+        pending.erase(pending.begin(), pending.begin() + done);
     }
     ~opose_ctx() {
+        if (nstream) {
+            (void)hipStreamSynchronize(nstream);
+            (void)hipStreamDestroy(nstream);
+        }
+        for (hipEvent_t e : {ev_net, ev_main, ev_post[0], ev_post[1]})
+            if (e) (void)hipEventDestroy(e);
         for (auto& kv : graphs)
             if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
         for (auto e : event_pool) (void)hipEventDestroy(e);
@@ -860,7 +892,7 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     const int ns = (int)gs.size();
     PafScales S{};
     for (int s = 0; s < ns; ++s) {
-        S.mid[s] = h->mids[s].ensure<float>(0, h->stream);
+        S.mid[s] = h->mid(s).ensure<float>(0, h->stream);
         S.hs[s] = gs[s].Hs;
         S.ws[s] = gs[s].Ws;
         S.sy[s] = gs[s].up_sy;
@@ -912,7 +944,7 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
 }
 
 static void upsample_to_mid(opose_ctx* h, int s, const float* maps, int cstride, int N, const ScaleGeom& g, int C) {
-    float* mid = h->mids[s].ensure<float>((size_t)N * C * g.Hs * g.Ws, h->stream);
+    float* mid = h->mid(s).ensure<float>((size_t)N * C * g.Hs * g.Ws, h->stream);
     ProfEntry pe;
     h->prof_begin(pe, "upsample8", 0, (double)N * C * g.Hs * g.Ws * 4);
     launch_upsample8(maps, cstride, 0, C, N, g.hl, g.wl, g.Hs, g.Ws, mid, h->stream);
@@ -931,6 +963,15 @@ static int worst_status(const uint8_t* rec, int N, size_t bytes) {
 }  // namespace opose
 
 // ======================================================================== C ABI
+namespace opose {
+// every entry point that enqueues work on the handle's stream (other than the pipelined body
+// path): select the device, and make the next pipelined network wait for that stream
+static void enter_main(opose_ctx* h) {
+    OPOSE_HIP_CHECK(hipSetDevice(h->device));
+    h->main_dirty = true;
+}
+}  // namespace opose
+
 #define OPOSE_TRY(h, ...)                      \
     try {                                      \
         __VA_ARGS__;                           \
@@ -954,7 +995,7 @@ static void batch_post_common(opose_ctx* h, int N, int H, int W, const float* ma
     const RecordLayout L = make_record_layout(h->ppp, h->maxp);
     const int cap = h->ppp;
     ProfEntry pe;
-    float* mid = h->mids[0].ensure<float>((size_t)N * 56 * nh * nw, h->stream);
+    float* mid = h->mid(0).ensure<float>((size_t)N * 56 * nh * nw, h->stream);
     h->prof_begin(pe, "upsample8", 0, (double)N * 56 * nh * nw * 4);
     launch_upsample8_torch(maps, cstride, 0, 56, N, hl, wl, nh, nw, mid, h->stream);
     h->prof_end(pe);
@@ -1111,7 +1152,10 @@ void* opose_get_stream(const opose_t* h) { return h ? h->stream : nullptr; }
 
 int opose_synchronize(opose_t* h) {
     if (!h) return OPOSE_E_ARG;
-    OPOSE_TRY(h, OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream)));
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+        if (h->nstream) OPOSE_HIP_CHECK(hipStreamSynchronize(h->nstream));
+    });
     return OPOSE_OK;
 }
 
@@ -1127,7 +1171,7 @@ size_t opose_body_record_bytes(const opose_t* h) { return h ? make_record_layout
 int opose_load_weights(opose_t* h, int net, const float* const* tensors, const int64_t* shapes, int n) {
     if (!h || !tensors || !shapes || (net != OPOSE_NET_BODY && net != OPOSE_NET_HAND)) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         const std::vector<Spec> order = state_dict_order(net);
         if ((size_t)n != 2 * order.size()) {
             h->err = "expected " + std::to_string(2 * order.size()) + " tensors, got " + std::to_string(n);
@@ -1179,7 +1223,7 @@ int opose_load_weights(opose_t* h, int net, const float* const* tensors, const i
 static int net_forward(opose_t* h, int net, const float* x, int N, int Hp, int Wp, float* o1, float* o2, int flags) {
     if (!h || !x || N <= 0 || Hp < 8 || Wp < 8 || Hp % 8 || Wp % 8) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         const size_t in_n = (size_t)N * 3 * Hp * Wp;
         const float* xd = x;
         if (!(flags & OPOSE_IN_DEVICE)) {
@@ -1239,12 +1283,52 @@ static opose_params fill_params(const opose_params* p, int net) {
     return q;
 }
 
+namespace opose {
+static void pipelined_body(opose_ctx* h, int N, int H, int W, const std::vector<ScaleGeom>& gs,
+                           const opose_params& p, uint8_t* rec, const std::function<void()>& net_part) {
+    if (!h->nstream) {
+        int lo = 0, hi = 0;
+        OPOSE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        // the network stream gets the higher priority: its conv grids should not wait for
+        // post-network workgroups that can run on whatever CUs are left
+        OPOSE_HIP_CHECK(hipStreamCreateWithPriority(&h->nstream, hipStreamNonBlocking, hi));
+        for (hipEvent_t* e : {&h->ev_net, &h->ev_main, &h->ev_post[0], &h->ev_post[1]})
+            OPOSE_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+    const int set = h->next_set;
+    h->next_set ^= 1;
+    if (h->post_pending[set]) OPOSE_HIP_CHECK(hipStreamWaitEvent(h->nstream, h->ev_post[set], 0));
+    if (h->main_dirty) {
+        OPOSE_HIP_CHECK(hipEventRecord(h->ev_main, h->stream));
+        OPOSE_HIP_CHECK(hipStreamWaitEvent(h->nstream, h->ev_main, 0));
+        h->main_dirty = false;
+    }
+    hipStream_t main = h->stream;
+    h->mid_set = set;
+    h->stream = h->nstream;
+    try {
+        net_part();
+    } catch (...) {
+        h->stream = main;
+        h->mid_set = 0;
+        throw;
+    }
+    h->stream = main;
+    OPOSE_HIP_CHECK(hipEventRecord(h->ev_net, h->nstream));
+    OPOSE_HIP_CHECK(hipStreamWaitEvent(main, h->ev_net, 0));
+    body_post_common(h, N, H, W, gs, p, rec);
+    OPOSE_HIP_CHECK(hipEventRecord(h->ev_post[set], main));
+    h->post_pending[set] = true;
+    h->mid_set = 0;
+}
+}  // namespace opose
+
 int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride, int64_t frame_stride,
                      const opose_params* pp, void* records, int flags) {
     if (!h || !bgr || !records || N <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
     if (row_stride < (int64_t)W * 3 || frame_stride < row_stride * H) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));  // pipelined or not: decided below
         const opose_params p = fill_params(pp, OPOSE_NET_BODY);
         const RecordLayout L = make_record_layout(h->ppp, h->maxp);
         const uint8_t* fd = bgr;
@@ -1257,8 +1341,7 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
         for (int s = 0; s < p.n_scales; ++s) gs.push_back(geom(p.scales[s], p, H, W));
         uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)
                                                   : h->records.ensure<uint8_t>(L.bytes * N, h->stream);
-        const std::string key = call_key("body", N, H, W, row_stride, frame_stride, p, fd, rec, h->ppp, h->maxp);
-        run_graphed(h, key, [&] {
+        auto net_part = [&] {
             for (int s = 0; s < p.n_scales; ++s) {
                 const ScaleGeom& g = gs[s];
                 float* x = h->x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
@@ -1270,8 +1353,18 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
                 float* S = body_net(h, x, N, g.Hp, g.Wp);
                 upsample_to_mid(h, s, S, 185, N, g, 56);
             }
-            body_post_common(h, N, H, W, gs, p, rec);
-        });
+        };
+        if (h->pipeline && (flags & OPOSE_PIPELINE) && (flags & OPOSE_IN_DEVICE) && (flags & OPOSE_OUT_DEVICE)) {
+            pipelined_body(h, N, H, W, gs, p, rec, net_part);
+        } else {
+            enter_main(h);
+            h->mid_set = 0;
+            const std::string key = call_key("body", N, H, W, row_stride, frame_stride, p, fd, rec, h->ppp, h->maxp);
+            run_graphed(h, key, [&] {
+                net_part();
+                body_post_common(h, N, H, W, gs, p, rec);
+            });
+        }
         return finish_records(h, N, records, rec, flags);
     });
 }
@@ -1281,7 +1374,7 @@ int opose_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int pa
     if (!h || !maps || !records || N <= 0 || hl <= 0 || wl <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
     if (pad_down < 0 || pad_right < 0 || pad_down >= 8 * hl || pad_right >= 8 * wl) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         opose_params p = fill_params(pp, OPOSE_NET_BODY);
         p.n_scales = 1;
         const RecordLayout L = make_record_layout(h->ppp, h->maxp);
@@ -1332,7 +1425,7 @@ int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, i
     if (!h || !bgr || !maps || N <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
     if (row_stride < (int64_t)W * 3 || frame_stride < row_stride * H) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         const opose_params p = fill_params(pp, OPOSE_NET_BODY);
         if (s < 0 || s >= p.n_scales) return OPOSE_E_ARG;
         const uint8_t* fd = bgr;
@@ -1368,7 +1461,7 @@ int opose_body_post_scales(opose_t* h, const float* const* maps, const int* hl, 
             pad_down[s] >= 8 * hl[s] || pad_right[s] >= 8 * wl[s])
             return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         opose_params p = fill_params(pp, OPOSE_NET_BODY);
         const RecordLayout L = make_record_layout(h->ppp, h->maxp);
         std::vector<ScaleGeom> gs;
@@ -1405,7 +1498,7 @@ int opose_batch_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, 
     if (!h || !bgr || !records || N <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
     if (row_stride < (int64_t)W * 3 || frame_stride < row_stride * H) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         const opose_params p = fill_params(pp, OPOSE_NET_BODY);
         const RecordLayout L = make_record_layout(h->ppp, h->maxp);
         // Batch_body.calculate_size_pad (srcmx/Batch_model.py:302-307): int() truncation
@@ -1441,7 +1534,7 @@ int opose_batch_body_post(opose_t* h, const float* maps, int N, int hl, int wl, 
     if (!h || !maps || !records || N <= 0 || hl <= 0 || wl <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
     if (nh <= 0 || nw <= 0 || nh > 8 * hl || nw > 8 * wl) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         const opose_params p = fill_params(pp, OPOSE_NET_BODY);
         const RecordLayout L = make_record_layout(h->ppp, h->maxp);
         const size_t n_in = (size_t)N * 57 * hl * wl;
@@ -1470,7 +1563,7 @@ static void hand_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     ProfEntry pe;
     for (int s = 0; s < ns; ++s) {
         h->prof_begin(pe, "heat_full", 0, (double)NP * H * W * 8 * (s ? 2 : 1));
-        const float* mid = h->mids[s].ensure<float>(0, h->stream) + (size_t)mid_crop * 21 * gs[s].Hs * gs[s].Ws;
+        const float* mid = h->mid(s).ensure<float>(0, h->stream) + (size_t)mid_crop * 21 * gs[s].Hs * gs[s].Ws;
         launch_heat_full(mid, 21, 0, 21, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx, ns, s > 0, avg,
                          h->stream);
         h->prof_end(pe);
@@ -1511,7 +1604,7 @@ int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
     if (!h || !bgr || !peaks || !found || N <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
     if (row_stride < (int64_t)W * 3 || frame_stride < row_stride * H) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         const opose_params p = fill_params(pp, OPOSE_NET_HAND);
         const uint8_t* fd = bgr;
         if (!(flags & OPOSE_IN_DEVICE)) {
@@ -1551,7 +1644,7 @@ static void batch_hand_post_common(opose_ctx* h, int N, int H, int W, const floa
                                    const opose_params& p, double* peaks, int32_t* found, int flags) {
     const int NP = N * 21;
     ProfEntry pe;
-    float* mid = h->mids[0].ensure<float>((size_t)NP * H * W, h->stream);
+    float* mid = h->mid(0).ensure<float>((size_t)NP * H * W, h->stream);
     h->prof_begin(pe, "upsample8", 0, (double)NP * H * W * 4);
     launch_upsample8_torch(maps, cstride, 0, 21, N, H / 8, W / 8, H, W, mid, h->stream);
     h->prof_end(pe);
@@ -1577,7 +1670,7 @@ int opose_batch_hand_post(opose_t* h, const float* maps, int N, int hl, int wl, 
                           int32_t* found, int flags) {
     if (!h || !maps || !peaks || !found || N <= 0 || hl <= 0 || wl <= 0) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         const opose_params p = fill_params(pp, OPOSE_NET_HAND);
         const size_t n_in = (size_t)N * 22 * hl * wl;
         const float* md = maps;
@@ -1596,7 +1689,7 @@ int opose_batch_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, 
     if (!h || !bgr || !peaks || !found || N <= 0 || H <= 0 || W <= 0 || H % 8 || W % 8) return OPOSE_E_ARG;
     if (row_stride < (int64_t)W * 3 || frame_stride < row_stride * H) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         const opose_params p = fill_params(pp, OPOSE_NET_HAND);
         const uint8_t* fd = bgr;
         if (!(flags & OPOSE_IN_DEVICE)) {
@@ -1623,7 +1716,7 @@ int opose_hand_infer_crops(opose_t* h, const uint8_t* const* crops, const int* s
     for (int i = 0; i < n; ++i)
         if (!crops[i] || sizes[i] <= 0 || row_strides[i] < (int64_t)sizes[i] * 3) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         const opose_params p = fill_params(pp, OPOSE_NET_HAND);
         const int ns = p.n_scales;
         // per-crop geometry; the network side (Hs, Ws, Hp, Wp per scale) must agree across crops
@@ -1686,7 +1779,7 @@ int opose_hand_post(opose_t* h, const float* const* maps, const int* hl, const i
         n_scales < 1 || n_scales > OPOSE_MAX_SCALES)
         return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         opose_params p = fill_params(pp, OPOSE_NET_HAND);
         std::vector<ScaleGeom> gs;
         for (int s = 0; s < n_scales; ++s) {
@@ -1722,7 +1815,7 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
                      int Cout, int ks, int pad, int relu, int mt, int pt, int splits, float* out) {
     if (!h || !x || !w || !b || !out || ks > 15 || pad > 7) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         Spec s{"debug", Cin, Cout, ks, pad};
         upload_conv(h, 0, "__debug__", {&s}, {w}, {b});
         DevConv* c = h->convs[0]["__debug__"].get();
@@ -1761,7 +1854,7 @@ int opose_debug_conv_x6(opose_t* h, const float* x, const float* w, const float*
                         int Cout, int ks, int pad, int relu, int mt, int pt, int splits, int out_x6, float* out) {
     if (!h || !x || !w || !b || !out || ks > 15 || pad > 7) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         Spec s{"debug", Cin, Cout, ks, pad};
         upload_conv(h, 0, "__debug__", {&s}, {w}, {b});
         DevConv* c = h->convs[0]["__debug__"].get();
@@ -1806,7 +1899,7 @@ int opose_debug_conv_x6_time(opose_t* h, int N, int Cin, int H, int W, int Cout,
                              int splits, int reps, float* ms) {
     if (!h || !ms || reps < 1 || ngroups < 1 || ngroups > 2) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         Spec s{"timing", Cin, Cout, ks, ks / 2};
         std::vector<float> w((size_t)Cout * Cin * ks * ks), b(Cout, 0.f);
         for (size_t i = 0; i < w.size(); ++i) w[i] = (float)((i * 2654435761u) % 2001) / 1000.f - 1.f;
@@ -1862,7 +1955,7 @@ int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, in
                           int splits, int ablate, int reps, float* ms) {
     if (!h || !ms || reps < 1 || ngroups < 1 || ngroups > 2) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         Spec s{"timing", Cin, Cout, ks, ks / 2};
         std::vector<float> w((size_t)Cout * Cin * ks * ks, 0.01f), b(Cout, 0.f);
         upload_conv(h, 0, "__timing__", {&s}, {w.data()}, {b.data()});
@@ -1924,7 +2017,7 @@ int opose_debug_preprocess(opose_t* h, const uint8_t* bgr, int H, int W, double 
                            int* HpWp) {
     if (!h || !bgr || !HpWp) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         opose_params p;
         opose_default_params(OPOSE_NET_BODY, &p);
         const ScaleGeom g = geom(scale, p, H, W);
@@ -1948,7 +2041,7 @@ int opose_debug_heat(opose_t* h, const float* maps, int hl, int wl, int pad_down
                      double* heat_avg, float* paf_mid) {
     if (!h || !maps || !heat_avg) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
-        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        enter_main(h);
         DevBuf min_;
         float* md = min_.ensure<float>((size_t)57 * hl * wl, h->stream);
         OPOSE_HIP_CHECK(hipMemcpyAsync(md, maps, (size_t)57 * hl * wl * 4, hipMemcpyHostToDevice, h->stream));
@@ -1958,11 +2051,11 @@ int opose_debug_heat(opose_t* h, const float* maps, int hl, int wl, int pad_down
         g.up_sx = 1.0 / ((double)W / g.Ws);
         upsample_to_mid(h, 0, md, 57, 1, g, 56);
         double* avg = h->avg.ensure<double>((size_t)18 * H * W, h->stream);
-        launch_heat_full(h->mids[0].ensure<float>(0, h->stream), 56, 38, 18, 1, g.Hs, g.Ws, H, W, g.up_sy, g.up_sx, 1, 0,
+        launch_heat_full(h->mid(0).ensure<float>(0, h->stream), 56, 38, 18, 1, g.Hs, g.Ws, H, W, g.up_sy, g.up_sx, 1, 0,
                          avg, h->stream);
         OPOSE_HIP_CHECK(hipMemcpyAsync(heat_avg, avg, (size_t)18 * H * W * 8, hipMemcpyDeviceToHost, h->stream));
         if (paf_mid)
-            OPOSE_HIP_CHECK(hipMemcpyAsync(paf_mid, h->mids[0].ensure<float>(0, h->stream),
+            OPOSE_HIP_CHECK(hipMemcpyAsync(paf_mid, h->mid(0).ensure<float>(0, h->stream),
                                            (size_t)38 * g.Hs * g.Ws * 4, hipMemcpyDeviceToHost, h->stream));
         OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
     });
@@ -1978,7 +2071,7 @@ int opose_profile_enable(opose_t* h, int enable) {
 
 int opose_profile_reset(opose_t* h) {
     if (!h) return OPOSE_E_ARG;
-    OPOSE_TRY(h, h->prof_drain());
+    OPOSE_TRY(h, h->prof_drain(true));
     h->agg.clear();
     return OPOSE_OK;
 }
@@ -1987,7 +2080,8 @@ int opose_profile_read(opose_t* h, char* buf, size_t len) {
     if (!h || !buf || !len) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
         OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
-        h->prof_drain();
+        if (h->nstream) OPOSE_HIP_CHECK(hipStreamSynchronize(h->nstream));
+        h->prof_drain(true);
     });
     std::string s = "{";
     bool first = true;

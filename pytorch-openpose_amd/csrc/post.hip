@@ -496,10 +496,17 @@ __global__ __launch_bounds__(256) void limb_greedy(const double* __restrict__ sc
 __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ conn, const int* __restrict__ conn_cnt,
                                                       const int* __restrict__ part_cnt, RecordLayout L,
                                                       uint8_t* __restrict__ records) {
-    extern __shared__ double s_sub[];  // [max_people][20]
+    // [max_people][20] subset rows, then the current limb's connections staged from global memory
+    // (score, both candidates' scores, candidate indices): the serial loop below reads LDS only
+    extern __shared__ double smem[];
     const int n = blockIdx.x;
     const int lane = threadIdx.x;
     const int cap = L.peaks_per_part, maxp = L.max_people;
+    double* s_sub = smem;
+    double* s_cs = smem + (size_t)maxp * 20;
+    double* s_sa = s_cs + cap;
+    double* s_sb = s_sa + cap;
+    int* s_ci = reinterpret_cast<int*>(s_sb + cap);
     uint8_t* rec = records + (size_t)n * L.bytes;
     int32_t* hdr = reinterpret_cast<int32_t*>(rec);
     const double* cand = reinterpret_cast<const double*>(rec + L.cand_off);
@@ -518,10 +525,20 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
         if (nc < 0) continue;
         const int ia = kLimbA[k], ib = kLimbB[k];
         const Conn* ck = conn + ((size_t)n * 19 + k) * cap;
+        for (int c = lane; c < nc; c += 64) {
+            const Conn cc = ck[c];
+            const int ga = s_start[ia] + cc.i, gb = s_start[ib] + cc.j;
+            s_cs[c] = cc.s;
+            s_sa[c] = cand[(size_t)ga * 4 + 2];
+            s_sb[c] = cand[(size_t)gb * 4 + 2];
+            s_ci[2 * c] = ga;
+            s_ci[2 * c + 1] = gb;
+        }
+        __syncthreads();
         for (int c = 0; c < nc; ++c) {
-            const double idA = (double)(s_start[ia] + ck[c].i);
-            const double idB = (double)(s_start[ib] + ck[c].j);
-            const double s = ck[c].s;
+            const double idA = (double)s_ci[2 * c];
+            const double idB = (double)s_ci[2 * c + 1];
+            const double s = s_cs[c];
             int found = 0, j1 = -1, j2 = -1;
             for (int r0 = 0; r0 < nrows; r0 += 64) {
                 const int r = r0 + lane;
@@ -543,7 +560,7 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
                 if (lane == 0 && s_sub[j1 * 20 + ib] != idB) {
                     s_sub[j1 * 20 + ib] = idB;
                     s_sub[j1 * 20 + 19] = s_sub[j1 * 20 + 19] + 1.0;
-                    s_sub[j1 * 20 + 18] = s_sub[j1 * 20 + 18] + (cand[(size_t)idB * 4 + 2] + s);
+                    s_sub[j1 * 20 + 18] = s_sub[j1 * 20 + 18] + (s_sb[c] + s);
                 }
             } else if (found == 2) {
                 const bool both = lane < 18 && s_sub[j1 * 20 + lane] >= 0.0 && s_sub[j2 * 20 + lane] >= 0.0;
@@ -563,7 +580,7 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
                 } else if (lane == 0) {
                     s_sub[j1 * 20 + ib] = idB;
                     s_sub[j1 * 20 + 19] = s_sub[j1 * 20 + 19] + 1.0;
-                    s_sub[j1 * 20 + 18] = s_sub[j1 * 20 + 18] + (cand[(size_t)idB * 4 + 2] + s);
+                    s_sub[j1 * 20 + 18] = s_sub[j1 * 20 + 18] + (s_sb[c] + s);
                 }
             } else if (k < 17) {
                 if (nrows >= maxp) {
@@ -575,13 +592,14 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
                     if (lane == ia) v = idA;
                     if (lane == ib) v = idB;
                     if (lane == 19) v = 2.0;
-                    if (lane == 18) v = (cand[(size_t)idA * 4 + 2] + cand[(size_t)idB * 4 + 2]) + s;
+                    if (lane == 18) v = (s_sa[c] + s_sb[c]) + s;
                     s_sub[nrows * 20 + lane] = v;
                 }
                 ++nrows;
             }
             __syncthreads();
         }
+        __syncthreads();  // the staged connections are re-filled by the next limb
     }
     // prune (src/body.py:203-208) and emit in order
     int kept = 0;
@@ -651,8 +669,16 @@ void launch_limb_greedy(const double* score, const int* part_cnt, int N, int cap
 
 void launch_assemble(const Conn* conn, const int* conn_cnt, const int* part_cnt, int N, const RecordLayout& L,
                      uint8_t* records, hipStream_t st) {
-    hipLaunchKernelGGL(assemble_people, dim3(N), dim3(64), sizeof(double) * 20 * L.max_people, st, conn, conn_cnt,
-                       part_cnt, L, records);
+    const size_t shm = sizeof(double) * 20 * L.max_people + (size_t)L.peaks_per_part * (3 * sizeof(double) + 2 * sizeof(int));
+    if (shm > 64 * 1024) {  // grown capacities (up to 256 people / 1024 peaks per part: 80 KB)
+        static size_t granted = 0;
+        if (shm > granted) {
+            OPOSE_HIP_CHECK(hipFuncSetAttribute((const void*)assemble_people,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+            granted = shm;
+        }
+    }
+    hipLaunchKernelGGL(assemble_people, dim3(N), dim3(64), shm, st, conn, conn_cnt, part_cnt, L, records);
 }
 
 }  // namespace opose

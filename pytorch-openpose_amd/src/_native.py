@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("OPOSE_LIB", os.path.join(os.path.dirname(_HERE), "lib
 OPOSE_OK = 0
 OPOSE_E_ARG, OPOSE_E_SHAPE, OPOSE_E_HIP, OPOSE_E_WEIGHTS, OPOSE_E_CAPACITY, OPOSE_E_ASSEMBLY = -1, -2, -3, -4, -5, -6
 NET_BODY, NET_HAND = 0, 1
-IN_DEVICE, OUT_DEVICE = 1, 2
+IN_DEVICE, OUT_DEVICE, PIPELINE = 1, 2, 4
 MAX_SCALES = 8
 
 

@@ -163,10 +163,13 @@ class Body(object):
             return [self._decode(r) for r in rec]
 
     # ------------------------------------------------------------------ device API
-    def infer_records(self, frames_dev, records_dev=None):
+    def infer_records(self, frames_dev, records_dev=None, pipeline=False):
         """frames_dev: torch.uint8 cuda [N,H,W,3]; returns a torch.uint8 cuda [N, record_bytes] tensor.
 
-        Asynchronous on the handle's stream (no host synchronisation)."""
+        Asynchronous on the handle's stream (no host synchronisation).  pipeline=True
+        (OPOSE_PIPELINE, include/opose.h): the frames are complete now and are not modified until
+        the handle's stream passes this call; the call's network then overlaps the previous
+        call's post-processing (video-batch throughput)."""
         import torch
         N, H, W, _ = frames_dev.shape
         rb = self.handle.record_bytes()
@@ -174,7 +177,8 @@ class Body(object):
             records_dev = torch.empty((N, rb), dtype=torch.uint8, device=frames_dev.device)
         rc = _native.lib.opose_body_infer(self.handle.h, frames_dev.data_ptr(), N, H, W, frames_dev.stride(1),
                                           frames_dev.stride(0), self.params, records_dev.data_ptr(),
-                                          _native.IN_DEVICE | _native.OUT_DEVICE)
+                                          _native.IN_DEVICE | _native.OUT_DEVICE
+                                          | (_native.PIPELINE if pipeline else 0))
         self.handle.check(rc)
         return records_dev
 

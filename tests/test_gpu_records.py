@@ -1,0 +1,64 @@
+"""GPU: the device-resident batch path (Body.infer_records, opose_body_infer with
+IN_DEVICE | OUT_DEVICE) that bench.py times, against the host-memory batch path (Body.batch:
+the same batch through the same network tiles), serial and pipelined (OPOSE_PIPELINE: each
+call's network overlaps the previous call's post-processing on a second stream; the x8 maps
+alternate between two buffer sets).  Bar: identical candidates and
+subsets (same kernels, same arithmetic; only the launch order across streams differs)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+H, W, B = 184, 328, 3
+
+
+@pytest.fixture(scope="module")
+def body():
+    from src.body import Body
+    from src.weights import BENCH_OUT_SCALE, seeded_state_dict
+    return Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE))
+
+
+@pytest.fixture(scope="module")
+def batches():
+    rng = np.random.default_rng(21)
+    return [rng.integers(0, 256, (B, H, W, 3), dtype=np.uint8) for _ in range(3)]
+
+
+@pytest.fixture(scope="module")
+def expected(body, batches):
+    return [body.batch(frames) for frames in batches]
+
+
+def _check(body, rec, exp):
+    got = body.decode_records(rec)
+    assert len(got) == len(exp)
+    for (c, s), (ec, es) in zip(got, exp):
+        assert np.array_equal(c, ec) and np.array_equal(s, es)
+
+
+def test_records_serial(body, batches, expected):
+    for frames, exp in zip(batches, expected):
+        rec = body.infer_records(torch.from_numpy(frames).cuda())
+        body.handle.synchronize()
+        _check(body, rec, exp)
+
+
+def test_records_pipelined(body, batches, expected):
+    dev = [torch.from_numpy(f).cuda() for f in batches]
+    torch.cuda.synchronize()  # frames complete before the pipelined calls (OPOSE_PIPELINE contract)
+    order = [0, 1, 2, 0, 1, 2, 1]
+    recs = [body.infer_records(dev[i], pipeline=True) for i in order]
+    body.handle.synchronize()
+    for i, rec in zip(order, recs):
+        _check(body, rec, expected[i])
+    # pipelined calls around a host-path call (shares the network workspace on the main stream)
+    r0 = body.infer_records(dev[2], pipeline=True)
+    mid = body.batch(batches[1])
+    r1 = body.infer_records(dev[0], pipeline=True)
+    body.handle.synchronize()
+    _check(body, r0, expected[2])
+    _check(body, r1, expected[0])
+    for (c, s), (ec, es) in zip(mid, expected[1]):
+        assert np.array_equal(c, ec) and np.array_equal(s, es)
