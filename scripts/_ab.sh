@@ -1,2 +1,3 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONDONTWRITEBYTECODE=1
-timeout -k 10 900 python -u scripts/bench_configs.py > gpurun_out/configs.json 2> gpurun_out/configs.err; rc=$?; tail -c 2000 gpurun_out/configs.json; tail -3 gpurun_out/configs.err; exit $rc
+AB_LAYERS=tiny3,tiny7_236,k7_c32 timeout -k 10 120 python scripts/x6_ab.py > gpurun_out/ab.log 2>&1; cat gpurun_out/ab.log
+AB_TILE=128x256 AB_LAYERS=tiny3 timeout -k 10 120 python scripts/x6_ab.py > gpurun_out/ab.log 2>&1; cat gpurun_out/ab.log

@@ -23,7 +23,9 @@ for name, N, Cin, H, W, Cout, ks, ng in [("Mconv2-5", 32, 128, 23, 41, 128, 7, 2
                                           ("stage1_3x3", 32, 128, 23, 41, 128, 3, 2),
                                           # K scan of the Mconv shape (intercept = per-launch fixed cost)
                                           ("k7_c32", 32, 32, 23, 41, 128, 7, 2), ("k7_c64", 32, 64, 23, 41, 128, 7, 2),
-                                          ("k7_c256", 32, 256, 23, 41, 128, 7, 2)]:
+                                          ("k7_c256", 32, 256, 23, 41, 128, 7, 2),
+                                          # tiny launches: per-launch overhead floor
+                                          ("tiny3", 1, 32, 8, 8, 128, 3, 1), ("tiny7_236", 32, 32, 23, 41, 128, 7, 2)]:
     if layers and name not in layers.split(","):
         continue
     flops = 2.0 * N * H * W * Cout * Cin * ks * ks * ng
