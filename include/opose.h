@@ -190,8 +190,10 @@ int opose_hand_post(opose_t* h, const float* const* maps, const int* hl, const i
                     const opose_params* p, double* peaks, int32_t* found, int flags);
 
 /* ---- measurement ---------------------------------------------------------------------- */
-/* When enabled, every kernel launch is bracketed by HIP events on the handle's stream and
- * accumulated per kernel class.  opose_profile_read writes one JSON object. */
+/* When enabled, every kernel launch is bracketed by HIP events on the stream it runs on and
+ * accumulated per kernel class.  enable: 0 off, 1 per class, 2 per class and per layer,
+ * 3 the 7x7 conv class only (the dominant kernel: bench.py's live roofline at ~1/4 of the
+ * event overhead).  opose_profile_read writes one JSON object. */
 int opose_profile_enable(opose_t* h, int enable);
 int opose_profile_reset(opose_t* h);
 int opose_profile_read(opose_t* h, char* buf, size_t len);

@@ -147,9 +147,9 @@ struct DevConv {
 struct ProfEntry {
     std::string cls;
     std::string detail;  // optional second aggregation key (per layer / tile choice)
-    double flops;
-    double bytes;
-    hipEvent_t e0, e1;
+    double flops = 0;
+    double bytes = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;  // null: not recorded (profiling off / filtered)
 };
 
 struct ProfAgg {
@@ -242,6 +242,7 @@ struct opose_ctx {
     // profiling
     bool prof = false;
     bool detail = false;  // per-layer aggregation (opose_profile_enable(h, 2))
+    bool prof_conv7_only = false;  // opose_profile_enable(h, 3)
     std::vector<ProfEntry> pending;
     std::map<std::string, ProfAgg> agg;
     std::vector<hipEvent_t> event_pool;
@@ -257,7 +258,7 @@ struct opose_ctx {
         return e;
     }
     void prof_begin(ProfEntry& pe, const char* cls, double flops, double bytes) {
-        if (!prof) return;
+        if (!prof || (prof_conv7_only && std::strcmp(cls, "conv7x7") != 0)) return;
         pe.cls = cls;
         pe.flops = flops;
         pe.bytes = bytes;
@@ -266,7 +267,7 @@ struct opose_ctx {
         OPOSE_HIP_CHECK(hipEventRecord(pe.e0, stream));
     }
     void prof_end(ProfEntry& pe) {
-        if (!prof) return;
+        if (!prof || !pe.e0) return;
         OPOSE_HIP_CHECK(hipEventRecord(pe.e1, stream));
         pending.push_back(pe);
     }
@@ -2065,7 +2066,8 @@ int opose_debug_heat(opose_t* h, const float* maps, int hl, int wl, int pad_down
 int opose_profile_enable(opose_t* h, int enable) {
     if (!h) return OPOSE_E_ARG;
     h->prof = enable != 0;
-    h->detail = enable >= 2;
+    h->detail = enable == 2;
+    h->prof_conv7_only = enable == 3;
     return OPOSE_OK;
 }
 
