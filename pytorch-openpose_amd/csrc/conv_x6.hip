@@ -92,7 +92,9 @@ template <int MT, int PT, bool SMALL, int KS, int MODE>
 __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int ks = KS ? KS : a.ks;
     const int taps = ks * ks;
-    constexpr int NW = x6_waves(MT, PT), NWM = NW == 8 ? MT / 64 : 2, NWP = NW / NWM;
+    // waves along M: 8-wave tiles and 64x256 (four 64x64 waves, the 128x256 tile's per-wave
+    // shape for M = 64 layers) one per 64 rows; the other 4-wave tiles 2 x 2
+    constexpr int NW = x6_waves(MT, PT), NWM = (NW == 8 || PT == 4 * MT) ? MT / 64 : 2, NWP = NW / NWM;
     constexpr int WM = MT / NWM, WP = PT / NWP;
     constexpr bool PIPE = MODE >= 1, S16 = MODE >= 2, BREG = MODE == 3;
     constexpr int MB = S16 ? 16 : 32;            // MFMA block (rows = pixels)
@@ -1071,6 +1073,7 @@ void launch_conv_x6(const X6Args& a, int mt, int pt, hipStream_t st) {
     else if (mt == 256 && pt == 128) launch_x6_tile<256, 128>(a, st);
     else if (mt == 128 && pt == 64) launch_x6_tile<128, 64>(a, st);
     else if (mt == 64 && pt == 128) launch_x6_tile<64, 128>(a, st);
+    else if (mt == 64 && pt == 256) launch_x6_tile<64, 256>(a, st);
     else if (mt == 64 && pt == 64) launch_x6_tile<64, 64>(a, st);
     else throw std::invalid_argument("unsupported x6 conv tile");
 }

@@ -325,12 +325,19 @@ struct TileChoice {
 // SIMD) runs at ~60 %.  Stream-K (grid = all resident slots) balances the chip exactly and
 // pays for the partial slabs of tiles it splits plus one fixup launch.
 TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false) {
-    static const int cfg[6][3] = {{128, 128, 2}, {128, 256, 1}, {256, 128, 1},
-                                  {128, 64, 3},  {64, 128, 3},  {64, 64, 4}};  // mt, pt, WG/CU
+    static const int cfg[7][3] = {{128, 128, 2}, {128, 256, 1}, {256, 128, 1}, {128, 64, 3},
+                                  {64, 128, 3},  {64, 64, 4},   {64, 256, 0}};  // mt, pt, WG/CU
     // split-bf16 kernel: 2.5x the MFMA rate per chunk, more LDS per workgroup
-    static const int occ6[6] = {1, 1, 1, 2, 2, 3};
-    // (256x128 measured 0-2.5 % faster than 128x256 where both fit: half the im2col DMA per MFMA)
-    static const double ovh6[6] = {1.5, 1.0, 0.96, 1.1, 1.1, 1.2};
+    static const int occ6[7] = {1, 1, 1, 2, 2, 3, 1};
+    // (256x128 measured 0-2.5 % faster than 128x256 where both fit: half the im2col DMA per MFMA;
+    // 64x256 = four 64x64 waves for the M = 64 layers, opt-in (OPOSE_X6_T64X256=1): conv1_2
+    // measured 91 vs 109 TF/s with 64x128 -- an M = 64 tile loads the same im2col bytes per MFMA
+    // whatever its width, and one workgroup per CU leaves one wave per SIMD (scripts/t64_ab.sh)
+    static const double ovh6[7] = {1.5, 1.0, 0.96, 1.1, 1.1, 1.2, 1.0};
+    static const bool t64x256 = [] {
+        const char* e = getenv("OPOSE_X6_T64X256");
+        return e && e[0] == '1';
+    }();
     const double rate = x6 ? 0.4 : 1.0;
     // relative cost per MFMA of the smaller tiles (more load/issue work per MFMA); measured
     // with scripts/conv_timing.py, overridable for A/B runs: OPOSE_TILE_OVH="1,.95,.93,1.02,1.02,1.06"
@@ -343,9 +350,9 @@ TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false)
     (void)ovh_env;
     TileChoice best{64, 64, 1};
     double best_cost = 1e300;
-    for (int c = 0; c < 6; ++c) {
+    for (int c = 0; c < (x6 ? 7 : 6); ++c) {  // 64x256 exists for the split-bf16 kernel only
         const int mt = cfg[c][0], pt = cfg[c][1], occ = x6 ? occ6[c] : cfg[c][2];
-        if (Mpad % mt) continue;
+        if (Mpad % mt || (c == 6 && !t64x256)) continue;
         const long tiles = (long)(Mpad / mt) * ((npix + pt - 1) / pt) * ngroups;
         const double unit = (mt / 64.0) * (pt / 64.0) * (x6 ? ovh6[c] : ovh[c]) * rate;
         // data parallel
