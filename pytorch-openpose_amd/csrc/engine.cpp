@@ -1299,7 +1299,9 @@ static void pipelined_body(opose_ctx* h, int N, int H, int W, const std::vector<
         OPOSE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
         // the network stream gets the higher priority: its conv grids should not wait for
         // post-network workgroups that can run on whatever CUs are left
-        OPOSE_HIP_CHECK(hipStreamCreateWithPriority(&h->nstream, hipStreamNonBlocking, hi));
+        // (OPOSE_NET_PRIORITY=0: the default priority, for A/B runs)
+        const char* pe = getenv("OPOSE_NET_PRIORITY");
+        OPOSE_HIP_CHECK(hipStreamCreateWithPriority(&h->nstream, hipStreamNonBlocking, pe && pe[0] == '0' ? lo : hi));
         for (hipEvent_t* e : {&h->ev_net, &h->ev_main, &h->ev_post[0], &h->ev_post[1]})
             OPOSE_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }

@@ -49,10 +49,14 @@ def test_records_pipelined(body, batches, expected):
     dev = [torch.from_numpy(f).cuda() for f in batches]
     torch.cuda.synchronize()  # frames complete before the pipelined calls (OPOSE_PIPELINE contract)
     order = [0, 1, 2, 0, 1, 2, 1]
-    recs = [body.infer_records(dev[i], pipeline=True) for i in order]
-    body.handle.synchronize()
-    for i, rec in zip(order, recs):
-        _check(body, rec, expected[i])
+    # repeated: a race that needs the post kernels to overlap a particular network layer shows
+    # up in a few frames per hundred (the opt-in screened NMS lost peaks this way), so one pass
+    # is not enough evidence
+    for _ in range(4):
+        recs = [body.infer_records(dev[i], pipeline=True) for i in order]
+        body.handle.synchronize()
+        for i, rec in zip(order, recs):
+            _check(body, rec, expected[i])
     # pipelined calls around a host-path call (shares the network workspace on the main stream)
     r0 = body.infer_records(dev[2], pipeline=True)
     mid = body.batch(batches[1])
