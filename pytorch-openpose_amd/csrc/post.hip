@@ -115,9 +115,8 @@ __device__ __forceinline__ bool gauss_tile(const T* __restrict__ m, int H, int W
 
 // tile id -> (x tile, y tile, map) with an XCD-contiguous order (guide T1): horizontally and
 // vertically adjacent tiles, which re-read each other's 13-pixel halos, share an L2.
-__device__ __forceinline__ void gauss_tile_coords(int H, int W, int& x0, int& y0, int& np) {
+__device__ __forceinline__ void gauss_tile_coords_of(int H, int W, int total, int b, int& x0, int& y0, int& np) {
     const int ntx = (W + TW - 1) / TW, nty = (H + TH - 1) / TH;
-    const int total = gridDim.x, b = blockIdx.x;
     const int q = total >> 3, rr = total & 7, xcd = b & 7;
     const int id = xcd * q + min(xcd, rr) + (b >> 3);
     const int tx = id % ntx, rest = id / ntx;
@@ -126,17 +125,24 @@ __device__ __forceinline__ void gauss_tile_coords(int H, int W, int& x0, int& y0
     x0 = tx * TW;
     y0 = ty * TH;
 }
+__device__ __forceinline__ void gauss_tile_coords(int H, int W, int& x0, int& y0, int& np) {
+    gauss_tile_coords_of(H, W, gridDim.x, blockIdx.x, x0, y0, np);
+}
 
 // avg: [N*P][H][W] (float32 single scale / float64 average); one workgroup per tile.
+// `tiles` = all tiles; a grid smaller than that loops over them (grid-strided, a multiple of 8 so
+// every workgroup stays on its XCD's contiguous tile range): a capped grid leaves CUs to the
+// pipelined network's large-LDS conv workgroups
 template <typename T>
-__global__ __launch_bounds__(256) void gauss_nms(const T* __restrict__ avg, int P, int H, int W, double thre,
+__global__ __launch_bounds__(256) void gauss_nms(const T* __restrict__ avg, int tiles, int H, int W, double thre,
                                                  int cap, int* __restrict__ cnt, int* __restrict__ list,
                                                  double* __restrict__ list_score) {
     __shared__ GaussTile t;
+    for (int b = blockIdx.x; b < tiles; b += gridDim.x) {
     int x0, y0, np;
-    gauss_tile_coords(H, W, x0, y0, np);
+    gauss_tile_coords_of(H, W, tiles, b, x0, y0, np);
     const T* m = avg + (size_t)np * H * W;
-    if (!gauss_tile(m, H, W, x0, y0, t, gauss_skip_below(thre))) return;  // no pixel can pass `> thre`
+    if (gauss_tile(m, H, W, x0, y0, t, gauss_skip_below(thre))) {  // else no pixel can pass `> thre`
     for (int e = threadIdx.x; e < TW * TH; e += 256) {
         const int r = e / TW, c = e - r * TW;
         const int y = y0 + r, x = x0 + c;
@@ -153,6 +159,9 @@ __global__ __launch_bounds__(256) void gauss_nms(const T* __restrict__ avg, int 
                 list_score[(size_t)np * cap + slot] = (double)m[(size_t)y * W + x];  // map_ori[y, x]
             }
         }
+    }
+    }
+    __syncthreads();  // t is refilled by the next tile
     }
 }
 
@@ -818,11 +827,18 @@ void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double th
                                thre, cap, cnt, list, list_score);
         return;
     }
+    // OPOSE_GAUSS_GRID=n (multiple of 8): at most n workgroups looping over the tiles
+    static const int gcap = [] {
+        const char* e = getenv("OPOSE_GAUSS_GRID");
+        return e ? (atoi(e) / 8) * 8 : 0;
+    }();
+    const int tiles = (int)grid.x;
+    const dim3 g2(gcap > 0 && gcap < tiles ? gcap : tiles);
     if (f32)
-        hipLaunchKernelGGL(gauss_nms<float>, grid, dim3(256), 0, st, (const float*)avg, 18, H, W, thre, cap, cnt, list,
-                           list_score);
+        hipLaunchKernelGGL(gauss_nms<float>, g2, dim3(256), 0, st, (const float*)avg, tiles, H, W, thre, cap, cnt,
+                           list, list_score);
     else
-        hipLaunchKernelGGL(gauss_nms<double>, grid, dim3(256), 0, st, (const double*)avg, 18, H, W, thre, cap, cnt,
+        hipLaunchKernelGGL(gauss_nms<double>, g2, dim3(256), 0, st, (const double*)avg, tiles, H, W, thre, cap, cnt,
                            list, list_score);
 }
 
