@@ -1132,7 +1132,13 @@ int opose_create(int device, opose_t** out) {
     *out = nullptr;
     auto* h = new opose_ctx();
     h->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    // OPOSE_POST_PRIORITY=1: the handle's own stream (the post-network kernels of a pipelined
+    // step) at the highest priority, for A/B runs against the default (network stream highest)
+    const char* pp = getenv("OPOSE_POST_PRIORITY");
+    int plo = 0, phi = 0;
+    const bool post_hi = pp && pp[0] == '1' && hipDeviceGetStreamPriorityRange(&plo, &phi) == hipSuccess;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithPriority(&h->own_stream, hipStreamNonBlocking, post_hi ? phi : 0) != hipSuccess) {
         delete h;
         return OPOSE_E_HIP;
     }
