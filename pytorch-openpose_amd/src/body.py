@@ -172,11 +172,16 @@ class Body(object):
         call's post-processing (video-batch throughput)."""
         import torch
         N, H, W, _ = frames_dev.shape
+        if frames_dev.stride(3) != 1 or frames_dev.stride(2) != 3:
+            frames_dev = frames_dev.contiguous()  # pixels must be packed BGR; rows / frames may be strided
+        # a size-1 axis may carry any stride (0 for a numpy newaxis): give it the dense one
+        row_stride = frames_dev.stride(1) if H > 1 else 3 * W
+        frame_stride = frames_dev.stride(0) if N > 1 else row_stride * H
         rb = self.handle.record_bytes()
         if records_dev is None:
             records_dev = torch.empty((N, rb), dtype=torch.uint8, device=frames_dev.device)
-        rc = _native.lib.opose_body_infer(self.handle.h, frames_dev.data_ptr(), N, H, W, frames_dev.stride(1),
-                                          frames_dev.stride(0), self.params, records_dev.data_ptr(),
+        rc = _native.lib.opose_body_infer(self.handle.h, frames_dev.data_ptr(), N, H, W, row_stride,
+                                          frame_stride, self.params, records_dev.data_ptr(),
                                           _native.IN_DEVICE | _native.OUT_DEVICE
                                           | (_native.PIPELINE if pipeline else 0))
         self.handle.check(rc)

@@ -66,3 +66,29 @@ def test_records_pipelined(body, batches, expected):
     _check(body, r1, expected[0])
     for (c, s), (ec, es) in zip(mid, expected[1]):
         assert np.array_equal(c, ec) and np.array_equal(s, es)
+
+
+def test_bench_frame_post_exact_vs_oracle(body):
+    """The bench's own configuration: a uniform-random 368x656 frame at scale 0.5 with the bench's
+    calibrated weights (crowded: ~300 peaks and ~20 people per frame).  The device path bench.py
+    times (infer_records) equals the GPU post-network path on the GPU network's maps, and that
+    equals the oracle's post-network restatement (src/body.py:52-212) on the same maps,
+    bit-exactly -- the post-processing half of the north-star bar at the benchmarked size."""
+    from oracle import body_post
+    from src.model import bodypose_model
+    from src.util import transfer
+    from src.weights import BENCH_OUT_SCALE, seeded_state_dict
+    img = np.random.default_rng(33).integers(0, 256, (368, 656, 3), dtype=np.uint8)
+    x, pad, padded_hw = body_post.preprocess(img, 0.5)
+    m = bodypose_model()
+    m.load_state_dict(transfer(m, seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE)))
+    paf, heat = m(x)
+    paf, heat = np.asarray(paf), np.asarray(heat)
+    cand, subset = body.post(np.concatenate([paf, heat], 1), list(pad), 368, 656)[0]
+    assert len(cand) > 100 and len(subset) > 5  # the crowded regime the bench measures
+    ref_c, ref_s = body_post.post_from_lowres((368, 656), [(paf[0], heat[0], list(pad), tuple(padded_hw))])
+    assert np.array_equal(cand, ref_c) and np.array_equal(subset, ref_s)
+    rec = body.infer_records(torch.from_numpy(img[None]).cuda())
+    body.handle.synchronize()
+    (dc, ds), = body.decode_records(rec)
+    assert np.array_equal(dc, cand) and np.array_equal(ds, subset)
