@@ -90,10 +90,14 @@ class Batch_body(Body):
         """Device-resident uint8 frames [N, H, W, 3] -> device records (asynchronous)."""
         import torch
         N, H, W, _ = frames_dev.shape
+        if frames_dev.stride(3) != 1 or frames_dev.stride(2) != 3:
+            frames_dev = frames_dev.contiguous()
+        row_stride = frames_dev.stride(1) if H > 1 else 3 * W  # size-1 axes: any stride (numpy newaxis: 0)
+        frame_stride = frames_dev.stride(0) if N > 1 else row_stride * H
         if records_dev is None:
             records_dev = torch.empty((N, self.handle.record_bytes()), dtype=torch.uint8, device=frames_dev.device)
         self.handle.check(_native.lib.opose_batch_body_infer(
-            self.handle.h, frames_dev.data_ptr(), N, H, W, frames_dev.stride(1), frames_dev.stride(0), self.params,
+            self.handle.h, frames_dev.data_ptr(), N, H, W, row_stride, frame_stride, self.params,
             records_dev.data_ptr(), _native.IN_DEVICE | _native.OUT_DEVICE))
         return records_dev
 
