@@ -109,6 +109,7 @@ __global__ __launch_bounds__(256) void cubic_resize_rows(const float* __restrict
                                                          float nscales, int accumulate, void* __restrict__ out,
                                                          int torch) {
     __shared__ float hs[MAXR][256];
+    __shared__ CubicTap s_ty[RS_RT];  // the vertical taps of this workgroup's rows, computed once
     const int tid = threadIdx.x;
     const int x = blockIdx.x * 256 + tid;
     const int y0 = blockIdx.y * RS_RT;
@@ -120,6 +121,7 @@ __global__ __launch_bounds__(256) void cubic_resize_rows(const float* __restrict
     const int r_lo = cubic_tap_any(y0, sy, hi, torch).i[0];
     const int r_hi = cubic_tap_any(y1 - 1, sy, hi, torch).i[3];
     const bool live = x < wo;
+    if (tid < y1 - y0) s_ty[tid] = cubic_tap_any(y0 + tid, sy, hi, torch);
     if (live) {
         const CubicTap tx = cubic_tap_any(x, sx, wi, torch);
         for (int r = r_lo; r <= r_hi; ++r) {
@@ -133,8 +135,9 @@ __global__ __launch_bounds__(256) void cubic_resize_rows(const float* __restrict
     }
     __syncthreads();
     if (!live) return;
+    const bool div = nscales != 1.f;  // x / 1.0f == x exactly: skip the IEEE division sequence
     for (int y = y0; y < y1; ++y) {
-        const CubicTap ty = cubic_tap_any(y, sy, hi, torch);
+        const CubicTap ty = s_ty[y - y0];
         float o = hs[ty.i[0] - r_lo][tid] * ty.c[0];
         o = o + hs[ty.i[1] - r_lo][tid] * ty.c[1];
         o = o + hs[ty.i[2] - r_lo][tid] * ty.c[2];
@@ -143,10 +146,10 @@ __global__ __launch_bounds__(256) void cubic_resize_rows(const float* __restrict
         if constexpr (MODE == 0) {
             reinterpret_cast<float*>(out)[e] = o;
         } else if constexpr (MODE == 1) {
-            reinterpret_cast<float*>(out)[e] = 0.f + o / nscales;
+            reinterpret_cast<float*>(out)[e] = 0.f + (div ? o / nscales : o);
         } else {
             double* d = reinterpret_cast<double*>(out) + e;
-            const float v = o / nscales;
+            const float v = div ? o / nscales : o;
             *d = accumulate ? *d + (double)v : 0.0 + (double)v;
         }
     }
