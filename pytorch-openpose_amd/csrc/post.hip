@@ -342,6 +342,59 @@ __global__ __launch_bounds__(256) void gauss_nms_screened(const T* __restrict__ 
     }
 }
 
+// Debug (OPOSE_GAUSS_DEBUG=1 with the screened kernel): the all-float64 kernel runs after it on the
+// same stream into shadow lists; one thread per map reports every peak of B missing from A with
+// the screen's float32 values at that pixel, recomputed in the screen's order.
+template <typename T>
+__global__ void gauss_debug_cmp(const T* __restrict__ avg, int NP, int H, int W, double thre, int cap,
+                                const int* cntA, const int* listA, const int* cntB, const int* listB) {
+    const int np = blockIdx.x * blockDim.x + threadIdx.x;
+    if (np >= NP) return;
+    const int na = min(cntA[np], cap), nb = min(cntB[np], cap);
+    const T* m = avg + (size_t)np * H * W;
+    for (int i = 0; i < nb; ++i) {
+        const int pb = listB[(size_t)np * cap + i];
+        bool found = false;
+        for (int j = 0; j < na; ++j) found |= listA[(size_t)np * cap + j] == pb;
+        if (found) continue;
+        const int y = pb / W, x = pb % W;
+        // footprint of the pixel's screened tile: max |input| (the screen's X)
+        const int x0 = (x / TW) * TW, y0 = (y / TH) * TH;
+        float X = 0.f;
+        for (int r = 0; r < GF_IR; ++r)
+            for (int c = 0; c < VW; ++c)
+                X = fmaxf(X, fabsf((float)m[(size_t)reflect_idx(y0 - 13 + r, H) * W + reflect_idx(x0 - 13 + c, W)]));
+        float w32[13];
+        for (int j = 0; j < 13; ++j) w32[j] = (float)kGauss[j];
+        float g[5];  // centre, up, down, left, right
+        const int dy[5] = {0, -1, 1, 0, 0}, dx[5] = {0, 0, 0, -1, 1};
+        for (int k = 0; k < 5; ++k) {
+            const int yy = y + dy[k], xx = x + dx[k];
+            float v[25];
+            for (int cc = 0; cc < 25; ++cc) {
+                const int col = reflect_idx(xx - 12 + cc, W);
+                float acc = (float)m[(size_t)reflect_idx(yy, H) * W + col] * w32[0];
+                for (int j = 12; j >= 1; --j)
+                    acc = acc + ((float)m[(size_t)reflect_idx(yy - j, H) * W + col] +
+                                 (float)m[(size_t)reflect_idx(yy + j, H) * W + col]) * w32[j];
+                v[cc] = acc;
+            }
+            float a = v[12] * w32[0];
+            for (int j = 12; j >= 1; --j) a = a + (v[12 - j] + v[12 + j]) * w32[j];
+            g[k] = a;
+        }
+        printf("GAUSSDBG map %d y %d x %d missing: cntA %d cntB %d  g32 %.9g up %.9g dn %.9g lf %.9g rt %.9g  X %.9g "
+               "thre %.9g in %.9g\n",
+               np, y, x, cntA[np], cntB[np], g[0], g[1], g[2], g[3], g[4], X, thre, (double)m[(size_t)y * W + x]);
+    }
+    for (int j = 0; j < na; ++j) {
+        const int pa = listA[(size_t)np * cap + j];
+        bool found = false;
+        for (int i = 0; i < nb; ++i) found |= listB[(size_t)np * cap + i] == pa;
+        if (!found) printf("GAUSSDBG map %d y %d x %d extra in screened\n", np, pa / W, pa % W);
+    }
+}
+
 // Hand: binary = gaussian_filter(map) > thre (src/hand.py:62-63) as union-find seeds:
 // lab[i] = start of i's run within its 64-pixel segment where set, -1 elsewhere; cnt[np] += #set.
 __global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict__ avg, int H, int W, double thre,
@@ -811,9 +864,11 @@ void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double th
                       double* list_score, hipStream_t st) {
     dim3 grid(((W + TW - 1) / TW) * ((H + TH - 1) / TH) * NP);
     // default: the all-float64 tile kernel.  OPOSE_GAUSS_SCREEN=1: float32 screen + exact
-    // re-evaluation -- exact when run alone, but it lost 1 strong peak in ~6 of 126 frames when
-    // its launches overlapped the pipelined network stream (scripts/pipeline_check.py; cause not
-    // found), and it gained nothing on the pipelined bench (1899 vs 1905 frames/s): opt-in only
+    // re-evaluation.  Its overlap-only peak loss (round 1) was the compiler's packed-FP32 code in
+    // the float32 horizontal pass: wrong low-element sums when the launch shared the chip with the
+    // pipelined network stream, exact alone; the library is now built without packed FP32
+    // (Makefile NOPK).  OPOSE_GAUSS_DEBUG=1 runs the float64 kernel after it into
+    // shadow lists and prints every difference from the device (scripts/gauss_debug.sh).
     static const bool screened = [] {
         const char* e = getenv("OPOSE_GAUSS_SCREEN");
         return e && e[0] == '1';
@@ -825,6 +880,34 @@ void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double th
         else
             hipLaunchKernelGGL(gauss_nms_screened<double>, grid, dim3(256), 0, st, (const double*)avg, 18, H, W,
                                thre, cap, cnt, list, list_score);
+        static const bool dbg = getenv("OPOSE_GAUSS_DEBUG") != nullptr;
+        if (dbg) {
+            static int* sh = nullptr;
+            static size_t sh_n = 0;
+            const size_t need = (size_t)NP * (cap + 1);
+            if (need > sh_n) {
+                OPOSE_HIP_CHECK(hipDeviceSynchronize());
+                if (sh) OPOSE_HIP_CHECK(hipFree(sh));
+                OPOSE_HIP_CHECK(hipMalloc(&sh, need * (4 + 8)));
+                sh_n = need;
+            }
+            int* c2 = sh;
+            int* l2 = sh + NP;
+            double* s2 = reinterpret_cast<double*>(sh + need + (need & 1));
+            OPOSE_HIP_CHECK(hipMemsetAsync(c2, 0, 4 * NP, st));
+            const int tiles = (int)grid.x;
+            if (f32) {
+                hipLaunchKernelGGL(gauss_nms<float>, grid, dim3(256), 0, st, (const float*)avg, tiles, H, W, thre, cap,
+                                   c2, l2, s2);
+                hipLaunchKernelGGL(gauss_debug_cmp<float>, dim3((NP + 63) / 64), dim3(64), 0, st, (const float*)avg,
+                                   NP, H, W, thre, cap, cnt, list, c2, l2);
+            } else {
+                hipLaunchKernelGGL(gauss_nms<double>, grid, dim3(256), 0, st, (const double*)avg, tiles, H, W, thre,
+                                   cap, c2, l2, s2);
+                hipLaunchKernelGGL(gauss_debug_cmp<double>, dim3((NP + 63) / 64), dim3(64), 0, st,
+                                   (const double*)avg, NP, H, W, thre, cap, cnt, list, c2, l2);
+            }
+        }
         return;
     }
     // OPOSE_GAUSS_GRID=n (multiple of 8): at most n workgroups looping over the tiles
