@@ -60,7 +60,25 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-iters", type=int, default=10)
     ap.add_argument("--detail", action="store_true", help="per-layer kernel times to stderr")
+    ap.add_argument("--host-steps", type=int, default=None,
+                    help="steps of the host-to-host pass (pinned frames in, records out over PCIe); default --steps")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: gloo ranks gather synthetic host records (tests the launcher and the gather)")
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without torchrun's environment: start N ranks (one per GPU) under
+    torch.distributed.run as a child process and exit with its status.  Nothing here touches the
+    GPU, so the child ranks own their devices from the start."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 # frames are resident and static for the whole run, so every step may overlap its network with
@@ -128,41 +146,152 @@ def stage_roofline(prof):
     return out
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(frames_np, seconds):
-    """Oracle (test infrastructure, used only as the timed CPU baseline) on whole frames."""
+    """Oracle (test infrastructure, used only as the timed CPU baseline) on whole frames.
+
+    Three bounded legs: the headline (C2 368x656 frames at the box's CPU share of threads, over
+    distinct frames), the same at 1 thread, and C1 (one 368x368 image, src/body.py on CPU)."""
     from oracle import body_post, network
     from src.weights import BENCH_OUT_SCALE
     # the box's CPU share for one GPU (OMP_NUM_THREADS is set to it there), not the whole machine
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
     sd = network.seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE)
 
     def net_fn(x):
         p, h = network.body_forward(torch.from_numpy(x), sd)
         return p.numpy(), h.numpy()
 
-    t0 = time.perf_counter()
-    n = 0
-    while True:
-        body_post.body_infer(frames_np[n % len(frames_np)], net_fn)
-        n += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
+    def timed(frames, secs, nthreads, min_frames=1):
+        torch.set_num_threads(nthreads)
+        t0 = time.perf_counter()
+        n = 0
+        while n < min_frames or time.perf_counter() - t0 < secs:
+            body_post.body_infer(frames[n % len(frames)], net_fn)
+            n += 1
+        return n, time.perf_counter() - t0
+
+    n, dt = timed(frames_np, seconds, threads)
+    n1, dt1 = timed(frames_np, seconds / 3, 1)
+    c1 = np.random.default_rng(7).integers(0, 256, (368, 368, 3), dtype=np.uint8)
+    nc, dtc = timed([c1], seconds / 3, threads)
+    torch.set_num_threads(threads)
     return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} frame(s) of 368x656 through oracle Body() (torch-CPU net + NumPy/SciPy post), "
-                      f"{dt:.1f} s, torch threads={threads}"}
+            "sample": f"{n} frame(s) of 368x656 ({min(n, len(frames_np))} distinct) through oracle Body() "
+                      f"(torch-CPU net + NumPy/SciPy post), {dt:.1f} s, torch threads={threads}",
+            "cpu_model": cpu_model(),
+            "one_thread": {"value": n1 / dt1, "unit": "frames/s", "cores": 1,
+                           "sample": f"{n1} frame(s) of 368x656, {dt1:.1f} s"},
+            "c1_368x368": {"value": nc / dtc, "unit": "frames/s", "cores": threads,
+                           "sample": f"{nc} run(s) of one 368x368 image (C1), {dtc:.1f} s"}}
+
+
+def dry_run(args, world, rank):
+    """CPU rehearsal of the multi-rank bench: gloo ranks, synthetic host records encoded per
+    frame, the same gather (src/dist.py) the GPU path runs over RCCL; checks frame order."""
+    import torch.distributed as dist
+    from src import _native
+    from src.dist import gather_records
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    B, ppp, maxp = args.batch, 8, 4
+    recs = []
+    for f in range(B):
+        fid = rank * B + f
+        recs.append(_native.encode_record([[fid, 0, 1.0, 0]], [[0] + [-1] * 17 + [1.0, 1]], ppp, maxp))
+    rec = torch.from_numpy(np.stack(recs))
+    t0 = time.perf_counter()
+    for _ in range(args.warmup + args.steps):
+        out = gather_records(rec, world * B, world)
+    dt = time.perf_counter() - t0
+    ids = [int(_native.decode_record(r.numpy(), ppp, maxp)[1][0, 0]) for r in out]
+    assert ids == list(range(world * B)), "gathered records out of frame order"
+    if rank == 0:
+        print(json.dumps({"metric": "frames/sec (body+PAF grouping) at 368x656", "dry_run": True,
+                          "value": world * B * (args.warmup + args.steps) / dt, "unit": "frames/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "frames_total": world * B * args.steps, "gathered_frames": len(ids)}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def host_to_host(body, frames_np, steps, dev, rank, world):
+    """PCIe-inclusive rate (the reference's boundary, src/body.py:44-50): pinned host frames
+    uploaded each step on a copy stream per frame buffer (double-buffered, overlapped with the
+    previous step's compute), records downloaded to pinned host memory each step."""
+    B = len(frames_np)
+    host = torch.from_numpy(frames_np).pin_memory()
+    rb = body.handle.record_bytes()
+    dbuf = [torch.empty_like(host, device=dev) for _ in range(2)]
+    rdev = [torch.empty((B, rb), dtype=torch.uint8, device=dev) for _ in range(2)]
+    rhost = [torch.empty((B, rb), dtype=torch.uint8).pin_memory() for _ in range(2)]
+    cps = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    lib_stream = torch.cuda.ExternalStream(body.handle.stream(), device=dev)
+    from src.dist import gather_records
+
+    def upload(i):
+        cps[i].wait_stream(lib_stream)  # the call that last read dbuf[i] has finished with it
+        with torch.cuda.stream(cps[i]):
+            dbuf[i].copy_(host, non_blocking=True)
+
+    def run(n):
+        for i in range(2):
+            upload(i)
+        for k in range(n):
+            i = k % 2
+            with torch.cuda.stream(cps[i]):  # the library waits for this buffer's upload only
+                body.infer_records(dbuf[i], rdev[i], pipeline=PIPELINE)
+            with torch.cuda.stream(lib_stream):
+                allrec = gather_records(rdev[i], world * B, world) if world > 1 else rdev[i]
+                if rank == 0:
+                    rhost[i].copy_(allrec[:B] if world > 1 else allrec, non_blocking=True)
+            if k + 2 < n:
+                upload(i)
+        body.handle.synchronize()
+        torch.cuda.synchronize()
+
+    run(2)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    return world * B * steps / dt, dt / steps * 1e3
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        return dry_run(args, world, rank)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -177,6 +306,7 @@ def main():
     rb = body.handle.record_bytes()
     rec = torch.empty((B, rb), dtype=torch.uint8, device=dev)
     lib_stream = torch.cuda.ExternalStream(body.handle.stream(), device=dev)
+    torch.cuda.synchronize()
     from src.dist import gather_records
 
     def step():
@@ -213,6 +343,10 @@ def main():
     dt = time.perf_counter() - t0
     prof_timed = body.handle.profile_read()
     body.handle.profile(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
     # per-stage breakdown: a separate profiled pass after the timed region, every launch
     # bracketed by events (the pipelined overlap inflates the post-network kernels' own times)
     prof_steps = max(2, min(args.steps, 5))
@@ -230,10 +364,8 @@ def main():
             tf = v["flops"] / (v["ms"] * 1e-3) / 1e12 if v["ms"] else 0
             print(f"{k:70s} {v['ms'] / prof_steps:8.3f} ms/step {tf:7.1f} TF/s", file=sys.stderr)
         prof = {k: v for k, v in prof.items() if not k.startswith("layer/")}
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
+    # host-to-host (PCIe-inclusive) pass: reported beside `value`, never as it
+    h2h_value, h2h_ms = host_to_host(body, frames_np, args.host_steps or args.steps, dev, rank, world)
 
     # single-frame latency (C2: one frame, host in -> host out through Body.__call__)
     lat = []
@@ -274,6 +406,12 @@ def main():
                        "net_input": [184, 328], "parallelism": f"frame-sharded dp{world}",
                        "step_overlap": "network of step k+1 overlaps post-processing of step k (OPOSE_PIPELINE)"
                        if PIPELINE else "none"},
+            "frames_total": frames_total,
+            "value_host_to_host": h2h_value,
+            "host_to_host": {"ms_per_step": h2h_ms, "basis": "pinned host frames uploaded each step on per-buffer "
+                             "copy streams (double-buffered, overlapped), records (and the RCCL gather when "
+                             "n_gpus > 1) downloaded to pinned host memory each step; reference boundary "
+                             "src/body.py:44-50"},
             "roofline": {"bound": "mfma", "kernel": CONV_KERNEL + " (7x7 CPM stages)",
                          "achieved": achieved, "peak": PEAK_CONV_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_CONV_TFLOPS,
@@ -292,8 +430,8 @@ def main():
             "mean_peaks_per_frame": float(counts[:, 0].mean()),
             "mean_people_per_frame": float(counts[:, 1].mean()),
         }
-        if not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(frames_np[:2], args.cpu_seconds)
+        if not args.no_cpu and world == 1:
+            out["cpu_baseline"] = cpu_baseline(frames_np[:8], args.cpu_seconds)
         print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

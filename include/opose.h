@@ -83,9 +83,22 @@ void opose_default_params(int net, opose_params* p);
 int opose_create(int device, opose_t** out);
 void opose_destroy(opose_t* h);
 const char* opose_last_error(const opose_t* h);
+/* The new stream is ordered after all work queued on the previous one (and on the pipelined
+ * network stream). */
 int opose_set_stream(opose_t* h, void* hip_stream);   /* NULL = the handle's own stream */
 void* opose_get_stream(const opose_t* h);
 int opose_synchronize(opose_t* h);
+/* Ordering against a caller's stream (e.g. the framework's current stream) for OPOSE_IN_DEVICE /
+ * OPOSE_OUT_DEVICE calls.  The reference computes synchronously on one device, so these replace
+ * the implicit ordering of its `torch.from_numpy(...).cuda()` / `.cpu()` round trips
+ * (src/body.py:44-50).
+ *   opose_wait_stream:   the handle's next work (either stream) starts after everything queued on
+ *                        `hip_stream` so far: device inputs produced there are complete.
+ *   opose_signal_stream: work queued on `hip_stream` from now on starts after everything queued
+ *                        on the handle's stream so far: device outputs are complete, and buffers
+ *                        the handle read can be freed or reused by `hip_stream`. */
+int opose_wait_stream(opose_t* h, void* hip_stream);
+int opose_signal_stream(opose_t* h, void* hip_stream);
 
 /* Capacity of one Body record: peaks kept per part and people kept per frame.
  * Defaults 96 / 96.  Overflow makes the frame's status OPOSE_E_CAPACITY. */

@@ -222,6 +222,11 @@ struct opose_ctx {
     }();
     hipStream_t nstream = nullptr;
     hipEvent_t ev_net = nullptr, ev_main = nullptr, ev_post[2] = {nullptr, nullptr};
+    // opose_wait_stream / opose_signal_stream / opose_set_stream: ordering against streams the
+    // caller owns (a framework's current stream); ev_ext is still to be waited on by `nstream`
+    // when that stream is created later
+    hipEvent_t ev_ext = nullptr, ev_sig = nullptr;
+    bool ext_for_nstream = false;
     bool post_pending[2] = {false, false};
     bool main_dirty = false;
     int mid_set = 0, next_set = 0;
@@ -299,7 +304,7 @@ struct opose_ctx {
             (void)hipStreamSynchronize(nstream);
             (void)hipStreamDestroy(nstream);
         }
-        for (hipEvent_t e : {ev_net, ev_main, ev_post[0], ev_post[1]})
+        for (hipEvent_t e : {ev_net, ev_main, ev_post[0], ev_post[1], ev_ext, ev_sig})
             if (e) (void)hipEventDestroy(e);
         for (auto& kv : graphs)
             if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
@@ -959,6 +964,12 @@ static void upsample_to_mid(opose_ctx* h, int s, const float* maps, int cstride,
     h->prof_end(pe);
 }
 
+// bytes a strided uint8 [N][H][W][3] host view spans: the last row ends 3*W bytes after its start,
+// so a view cut from the bottom-right of a larger buffer is never read past its end
+static size_t host_span(int N, int H, int W, int64_t row_stride, int64_t frame_stride) {
+    return (size_t)(N - 1) * (size_t)frame_stride + (size_t)(H - 1) * (size_t)row_stride + (size_t)W * 3;
+}
+
 static int worst_status(const uint8_t* rec, int N, size_t bytes) {
     int w = 0;
     for (int n = 0; n < N; ++n) {
@@ -1156,9 +1167,62 @@ void opose_destroy(opose_t* h) {
 
 const char* opose_last_error(const opose_t* h) { return h ? h->err.c_str() : "null handle"; }
 
+namespace opose {
+static hipEvent_t lazy_event(hipEvent_t& e) {
+    if (!e) OPOSE_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+}
+}  // namespace opose
+
 int opose_set_stream(opose_t* h, void* s) {
     if (!h) return OPOSE_E_ARG;
-    h->stream = s ? static_cast<hipStream_t>(s) : h->own_stream;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const hipStream_t ns = s ? static_cast<hipStream_t>(s) : h->own_stream;
+        if (ns != h->stream) {
+            // work still queued on the old stream (and on the pipelined network stream) uses the
+            // workspace the new stream's calls reuse: order the new stream after both
+            hipEvent_t e = lazy_event(h->ev_sig);
+            OPOSE_HIP_CHECK(hipEventRecord(e, h->stream));
+            OPOSE_HIP_CHECK(hipStreamWaitEvent(ns, e, 0));
+            if (h->nstream) {
+                OPOSE_HIP_CHECK(hipEventRecord(e, h->nstream));
+                OPOSE_HIP_CHECK(hipStreamWaitEvent(ns, e, 0));
+            }
+            h->stream = ns;
+            h->main_dirty = true;  // the next pipelined network waits for the new stream
+        }
+    });
+    return OPOSE_OK;
+}
+
+int opose_wait_stream(opose_t* h, void* s) {
+    if (!h) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const hipStream_t xs = static_cast<hipStream_t>(s);
+        if (xs == h->stream) return OPOSE_OK;
+        hipEvent_t e = lazy_event(h->ev_ext);
+        OPOSE_HIP_CHECK(hipEventRecord(e, xs));
+        OPOSE_HIP_CHECK(hipStreamWaitEvent(h->stream, e, 0));
+        if (h->nstream)
+            OPOSE_HIP_CHECK(hipStreamWaitEvent(h->nstream, e, 0));
+        else
+            h->ext_for_nstream = true;
+    });
+    return OPOSE_OK;
+}
+
+int opose_signal_stream(opose_t* h, void* s) {
+    if (!h) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const hipStream_t xs = static_cast<hipStream_t>(s);
+        if (xs == h->stream) return OPOSE_OK;
+        hipEvent_t e = lazy_event(h->ev_sig);
+        OPOSE_HIP_CHECK(hipEventRecord(e, h->stream));
+        OPOSE_HIP_CHECK(hipStreamWaitEvent(xs, e, 0));
+    });
     return OPOSE_OK;
 }
 
@@ -1311,6 +1375,10 @@ static void pipelined_body(opose_ctx* h, int N, int H, int W, const std::vector<
         for (hipEvent_t* e : {&h->ev_net, &h->ev_main, &h->ev_post[0], &h->ev_post[1]})
             OPOSE_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
+    if (h->ext_for_nstream) {  // an opose_wait_stream before this stream existed
+        OPOSE_HIP_CHECK(hipStreamWaitEvent(h->nstream, h->ev_ext, 0));
+        h->ext_for_nstream = false;
+    }
     const int set = h->next_set;
     h->next_set ^= 1;
     if (h->post_pending[set]) OPOSE_HIP_CHECK(hipStreamWaitEvent(h->nstream, h->ev_post[set], 0));
@@ -1350,7 +1418,8 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
         const uint8_t* fd = bgr;
         if (!(flags & OPOSE_IN_DEVICE)) {
             uint8_t* buf = h->frames.ensure<uint8_t>((size_t)frame_stride * N, h->stream);
-            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, (size_t)frame_stride * N, hipMemcpyHostToDevice, h->stream));
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, host_span(N, H, W, row_stride, frame_stride),
+                                           hipMemcpyHostToDevice, h->stream));
             fd = buf;
         }
         std::vector<ScaleGeom> gs;
@@ -1447,7 +1516,8 @@ int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, i
         const uint8_t* fd = bgr;
         if (!(flags & OPOSE_IN_DEVICE)) {
             uint8_t* buf = h->frames.ensure<uint8_t>((size_t)frame_stride * N, h->stream);
-            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, (size_t)frame_stride * N, hipMemcpyHostToDevice, h->stream));
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, host_span(N, H, W, row_stride, frame_stride),
+                                           hipMemcpyHostToDevice, h->stream));
             fd = buf;
         }
         const ScaleGeom g = geom(p.scales[s], p, H, W);
@@ -1525,7 +1595,8 @@ int opose_batch_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, 
         const uint8_t* fd = bgr;
         if (!(flags & OPOSE_IN_DEVICE)) {
             uint8_t* buf = h->frames.ensure<uint8_t>((size_t)frame_stride * N, h->stream);
-            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, (size_t)frame_stride * N, hipMemcpyHostToDevice, h->stream));
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, host_span(N, H, W, row_stride, frame_stride),
+                                           hipMemcpyHostToDevice, h->stream));
             fd = buf;
         }
         uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)
@@ -1625,7 +1696,8 @@ int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
         const uint8_t* fd = bgr;
         if (!(flags & OPOSE_IN_DEVICE)) {
             uint8_t* buf = h->frames.ensure<uint8_t>((size_t)frame_stride * N, h->stream);
-            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, (size_t)frame_stride * N, hipMemcpyHostToDevice, h->stream));
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, host_span(N, H, W, row_stride, frame_stride),
+                                           hipMemcpyHostToDevice, h->stream));
             fd = buf;
         }
         std::vector<ScaleGeom> gs;
@@ -1710,7 +1782,8 @@ int opose_batch_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, 
         const uint8_t* fd = bgr;
         if (!(flags & OPOSE_IN_DEVICE)) {
             uint8_t* buf = h->frames.ensure<uint8_t>((size_t)frame_stride * N, h->stream);
-            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, (size_t)frame_stride * N, hipMemcpyHostToDevice, h->stream));
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, host_span(N, H, W, row_stride, frame_stride),
+                                           hipMemcpyHostToDevice, h->stream));
             fd = buf;
         }
         // ToTensor - 0.5 at scale 1 (torch bicubic at scale 1 is the identity)
@@ -1751,8 +1824,8 @@ int opose_hand_infer_crops(opose_t* h, const uint8_t* const* crops, const int* s
         if (!(flags & OPOSE_IN_DEVICE)) {
             buf = h->frames.ensure<uint8_t>(off[n], h->stream);
             for (int i = 0; i < n; ++i)
-                OPOSE_HIP_CHECK(hipMemcpyAsync(buf + off[i], crops[i], off[i + 1] - off[i], hipMemcpyHostToDevice,
-                                               h->stream));
+                OPOSE_HIP_CHECK(hipMemcpyAsync(buf + off[i], crops[i], host_span(1, sizes[i], sizes[i], row_strides[i], 0),
+                                               hipMemcpyHostToDevice, h->stream));
         }
         for (int s = 0; s < ns; ++s) {
             const ScaleGeom& g0 = gs[0][s];

@@ -38,6 +38,8 @@ def _load():
         "opose_destroy": (None, [P]),
         "opose_last_error": (C.c_char_p, [P]),
         "opose_set_stream": (I, [P, P]),
+        "opose_wait_stream": (I, [P, P]),
+        "opose_signal_stream": (I, [P, P]),
         "opose_get_stream": (P, [P]),
         "opose_synchronize": (I, [P]),
         "opose_set_capacity": (I, [P, I, I]),
@@ -78,6 +80,7 @@ def _load():
 lib = _load()
 
 EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last_error", "opose_set_stream",
+            "opose_wait_stream", "opose_signal_stream",
             "opose_get_stream", "opose_synchronize", "opose_set_capacity", "opose_body_record_bytes",
             "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_body_infer",
             "opose_body_post", "opose_body_scale_geom", "opose_body_scale_maps",
@@ -124,6 +127,17 @@ class Handle:
             raise OposeError(rc, "opose_create failed (no usable HIP device?)")
         self.h = h
         self.device = device
+        # The handle's main stream is a torch pool stream (torch never destroys those): tensors
+        # whose last use is queued there (Handle.hold -> record_stream) can then be freed at any
+        # time, even after this handle is gone, without the allocator touching a dead stream.
+        self._torch_stream_obj = None
+        try:
+            import torch
+            if torch.cuda.is_available():
+                self._torch_stream_obj = torch.cuda.Stream(device=torch.device("cuda", device))
+                self.set_stream(self._torch_stream_obj.cuda_stream)
+        except ImportError:
+            pass
 
     def close(self):
         if getattr(self, "h", None):
@@ -156,6 +170,29 @@ class Handle:
 
     def synchronize(self):
         self.check(lib.opose_synchronize(self.h))
+
+    # ---- ordering against torch's current stream (every device-tensor entry point)
+    def _torch_stream(self):
+        import torch
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream or None)
+
+    def wait_torch(self):
+        """The handle's next work starts after everything queued on torch's current stream."""
+        self.check(lib.opose_wait_stream(self.h, self._torch_stream()))
+
+    def signal_torch(self):
+        """Torch's current stream continues after everything queued on the handle: outputs are
+        complete for torch consumers and the inputs the handle read may be freed/reused."""
+        self.check(lib.opose_signal_stream(self.h, self._torch_stream()))
+
+    def hold(self, *tensors):
+        """Keep the caching allocator from reusing these tensors' memory until the handle's
+        stream passes this point (asynchronous calls whose outputs stay on the handle's stream)."""
+        st = self._torch_stream_obj
+        if st is None or st.cuda_stream != self.stream():
+            raise RuntimeError("Handle.hold needs the handle on its torch pool stream (set_stream changed it)")
+        for t in tensors:
+            t.record_stream(st)
 
     # ---- weights
     def load_weights(self, net: int, tensors):

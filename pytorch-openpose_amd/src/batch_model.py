@@ -96,9 +96,11 @@ class Batch_body(Body):
         frame_stride = frames_dev.stride(0) if N > 1 else row_stride * H
         if records_dev is None:
             records_dev = torch.empty((N, self.handle.record_bytes()), dtype=torch.uint8, device=frames_dev.device)
+        self.handle.wait_torch()
         self.handle.check(_native.lib.opose_batch_body_infer(
             self.handle.h, frames_dev.data_ptr(), N, H, W, row_stride, frame_stride, self.params,
             records_dev.data_ptr(), _native.IN_DEVICE | _native.OUT_DEVICE))
+        self.handle.signal_torch()
         return records_dev
 
 

@@ -109,7 +109,7 @@ class Body(object):
         """Network maps of scale index `s` only: [N, 57, hl, wl] float32 (PAF 38 | heat 19).
 
         frames: uint8 [N,H,W,3] numpy (-> numpy) or a torch cuda tensor (-> torch cuda tensor,
-        written into `out` when given; the handle's stream is synchronised before returning)."""
+        written into `out` when given, complete in torch's current-stream order)."""
         if hasattr(frames, "data_ptr"):
             import torch
             if frames.dim() == 3:
@@ -121,10 +121,11 @@ class Body(object):
             if out is None:
                 out = torch.empty((N, 57, hl, wl), dtype=torch.float32, device=frames.device)
             assert out.is_contiguous() and tuple(out.shape) == (N, 57, hl, wl)
+            self.handle.wait_torch()
             self.handle.check(_native.lib.opose_body_scale_maps(
                 self.handle.h, frames.data_ptr(), N, H, W, frames.stride(1), max(frames.stride(0), frames.stride(1) * H),
                 self.params, s, out.data_ptr(), _native.IN_DEVICE | _native.OUT_DEVICE))
-            self.handle.check(_native.lib.opose_synchronize(self.handle.h))
+            self.handle.signal_torch()  # `out` complete in torch's stream order (e.g. an isend)
             return out
         frames = np.ascontiguousarray(frames if np.ndim(frames) == 4 else np.asarray(frames)[None])
         N, H, W, _ = frames.shape
@@ -150,6 +151,8 @@ class Body(object):
         N = maps[0].shape[0]
         ns = len(maps)
         ptrs = (ctypes.c_void_p * ns)(*[m.data_ptr() if dev else m.ctypes.data for m in maps])
+        if dev:
+            self.handle.wait_torch()  # e.g. maps received by an irecv on torch's stream
         arr = [(ctypes.c_int * ns)(*[g[i] for g in geoms]) for i in range(4)]
         while True:
             rec = np.empty((N, self.handle.record_bytes()), np.uint8)
@@ -166,7 +169,9 @@ class Body(object):
     def infer_records(self, frames_dev, records_dev=None, pipeline=False):
         """frames_dev: torch.uint8 cuda [N,H,W,3]; returns a torch.uint8 cuda [N, record_bytes] tensor.
 
-        Asynchronous on the handle's stream (no host synchronisation).  pipeline=True
+        Asynchronous (no host synchronisation): ordered after torch's current stream, and the
+        records are complete in that stream's order on return (opose_wait_stream /
+        opose_signal_stream).  pipeline=True
         (OPOSE_PIPELINE, include/opose.h): the frames are complete now and are not modified until
         the handle's stream passes this call; the call's network then overlaps the previous
         call's post-processing (video-batch throughput)."""
@@ -180,16 +185,26 @@ class Body(object):
         rb = self.handle.record_bytes()
         if records_dev is None:
             records_dev = torch.empty((N, rb), dtype=torch.uint8, device=frames_dev.device)
+        self.handle.wait_torch()  # frames / records produced or last used on torch's stream
         rc = _native.lib.opose_body_infer(self.handle.h, frames_dev.data_ptr(), N, H, W, row_stride,
                                           frame_stride, self.params, records_dev.data_ptr(),
                                           _native.IN_DEVICE | _native.OUT_DEVICE
                                           | (_native.PIPELINE if pipeline else 0))
         self.handle.check(rc)
+        if pipeline:
+            # outputs stay in the handle's stream order (torch's stream must not wait for them, or
+            # the next call's network could not overlap this call's post-processing): consumers
+            # order themselves on handle.stream() (bench.py, src/dist.py) or call decode_records
+            self.handle.hold(records_dev, frames_dev)
+        else:
+            self.handle.signal_torch()
         return records_dev
 
     def decode_records(self, records):
         """uint8 [N, record_bytes] (numpy or torch) -> list of (candidate, subset)."""
         if hasattr(records, "cpu"):
+            if records.is_cuda:
+                self.handle.signal_torch()  # pipelined records complete on the handle's stream
             records = records.cpu().numpy()
         return [self._decode(r) for r in np.asarray(records)]
 

@@ -121,9 +121,10 @@ class bodypose_model(_DeviceNet):
             xt = x.contiguous().float()
             paf = torch.empty((N, 38, H // 8, W // 8), device=x.device)
             heat = torch.empty((N, 19, H // 8, W // 8), device=x.device)
+            self.handle.wait_torch()  # xt may still be in flight on torch's stream
             self.handle.check(_native.lib.opose_body_forward(self.handle.h, xt.data_ptr(), N, H, W, paf.data_ptr(),
                                                              heat.data_ptr(), _native.IN_DEVICE | _native.OUT_DEVICE))
-            self.handle.synchronize()
+            self.handle.signal_torch()  # outputs ready (and xt free to reuse) in torch's stream order
             return paf, heat
         xn = np.ascontiguousarray(x.numpy() if hasattr(x, "numpy") else x, dtype=np.float32)
         paf = np.empty((N, 38, H // 8, W // 8), np.float32)
@@ -146,9 +147,10 @@ class handpose_model(_DeviceNet):
             import torch
             xt = x.contiguous().float()
             heat = torch.empty((N, 22, H // 8, W // 8), device=x.device)
+            self.handle.wait_torch()
             self.handle.check(_native.lib.opose_hand_forward(self.handle.h, xt.data_ptr(), N, H, W, heat.data_ptr(),
                                                              _native.IN_DEVICE | _native.OUT_DEVICE))
-            self.handle.synchronize()
+            self.handle.signal_torch()
             return heat
         xn = np.ascontiguousarray(x.numpy() if hasattr(x, "numpy") else x, dtype=np.float32)
         heat = np.empty((N, 22, H // 8, W // 8), np.float32)

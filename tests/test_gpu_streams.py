@@ -1,0 +1,107 @@
+"""GPU: ordering against torch's current stream (opose_wait_stream / opose_signal_stream) and the
+host-copy span of strided views.
+
+* Inputs produced asynchronously on a torch side stream (behind a spin kernel) are read only
+  after that stream gets there: Body.infer_records, the model forward on a `.half()` input.
+* The screened Gaussian NMS under pipelined overlap (its round-1 overlap-only peak loss, now
+  fixed by building without packed FP32) -- in a child process, as the kernel
+  choice is read from the environment once per process.
+* A bottom-right crop view that ends exactly at a PROT_NONE guard page: the host -> device
+  staging copy must not read past the view's last pixel (include/opose.h host pointers)."""
+import ctypes
+import mmap
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def body():
+    from src.body import Body
+    from src.weights import BENCH_OUT_SCALE, seeded_state_dict
+    return Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE))
+
+
+def _same(got, exp):
+    assert len(got) == len(exp)
+    for (c, s), (ec, es) in zip(got, exp):
+        assert np.array_equal(c, ec) and np.array_equal(s, es)
+
+
+def test_infer_records_waits_for_torch_stream(body):
+    frames = np.random.default_rng(5).integers(0, 256, (2, 184, 328, 3), dtype=np.uint8)
+    exp = body.batch(frames)
+    src = torch.from_numpy(frames).cuda()
+    dst = torch.zeros_like(src)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(50_000_000)  # the frames land only after this spin
+        dst.copy_(src)
+        rec = body.infer_records(dst)
+        got = body.decode_records(rec)
+    _same(got, exp)
+    with torch.cuda.stream(side):  # pipelined: the network stream waits too
+        torch.cuda._sleep(50_000_000)
+        dst.zero_()
+        dst.copy_(src)
+        rec = body.infer_records(dst, pipeline=True)
+    _same(body.decode_records(rec), exp)
+
+
+def test_forward_waits_for_half_input(body):
+    x = torch.from_numpy(np.random.default_rng(6).standard_normal((1, 3, 64, 96)).astype(np.float32))
+    xh = x.half()
+    paf_ref, heat_ref = body.model.forward(xh.float().numpy())
+    src = xh.cuda()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(50_000_000)
+        xd = src * 1  # produced on the side stream after the spin
+        paf, heat = body.model.forward(xd)
+        paf, heat = paf.cpu().numpy(), heat.cpu().numpy()
+    assert np.array_equal(paf, paf_ref) and np.array_equal(heat, heat_ref)
+
+
+def test_screened_nms_pipelined_exact():
+    env = dict(os.environ, OPOSE_GAUSS_SCREEN="1", OPOSE_GAUSS_DEBUG="1", PYTHONDONTWRITEBYTECODE="1")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "scripts", "pipeline_check.py")], cwd=REPO, env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    bad = [l for l in out.stdout.splitlines() if " frame " in l or "GAUSSDBG" in l]
+    assert not bad, "\n".join(bad[:10])
+    assert out.stdout.strip().endswith("done")
+
+
+def test_host_copy_stops_at_view_end(body):
+    """The view's last byte is the last byte before a PROT_NONE page."""
+    H, W, page = 96, 128, mmap.PAGESIZE
+    full_w = W + 40
+    nbytes = (H + 20) * full_w * 3
+    span = (nbytes + page - 1) // page * page
+    buf = mmap.mmap(-1, span + page, prot=mmap.PROT_READ | mmap.PROT_WRITE)
+    libc = ctypes.CDLL(None)
+    addr = ctypes.addressof(ctypes.c_char.from_buffer(buf))
+    assert libc.mprotect(ctypes.c_void_p(addr + span), page, 0) == 0  # guard page
+    try:
+        # image rows end exactly at the guard: place the (H+20) x full_w image at span - nbytes
+        img = np.frombuffer(buf, np.uint8, count=nbytes, offset=span - nbytes).reshape(H + 20, full_w, 3)
+        img[:] = np.random.default_rng(8).integers(0, 256, img.shape, dtype=np.uint8)
+        view = img[20:, 40:]  # bottom-right crop: its last pixel is the buffer's last byte
+        assert view.ctypes.data + (H - 1) * view.strides[0] + 3 * W == addr + span
+        got = body(view)
+        exp = body(np.ascontiguousarray(view))
+        _same([got], [exp])
+    finally:
+        libc.mprotect(ctypes.c_void_p(addr + span), page, mmap.PROT_READ | mmap.PROT_WRITE)
+        del img, view
+        buf.close()
