@@ -225,6 +225,13 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def max_over_ranks(x, dev):
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def host_to_host(body, frames_np, steps, dev, rank, world):
     """PCIe-inclusive rate (the reference's boundary, src/body.py:44-50): pinned host frames
     uploaded each step on a copy stream per frame buffer (double-buffered, overlapped with the
@@ -270,9 +277,7 @@ def host_to_host(body, frames_np, steps, dev, rank, world):
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = max_over_ranks(dt, dev)
     return world * B * steps / dt, dt / steps * 1e3
 
 
@@ -287,10 +292,18 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if args.dry_run:
         return dry_run(args, world, rank)
+    # one rank per GPU; BENCH_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
+    # per GPU (device = local rank modulo the visible GPUs, records gathered through the host)
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         world = dist.get_world_size()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -344,9 +357,7 @@ def main():
     prof_timed = body.handle.profile_read()
     body.handle.profile(False)
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = max_over_ranks(dt, dev)
     # per-stage breakdown: a separate profiled pass after the timed region, every launch
     # bracketed by events (the pipelined overlap inflates the post-network kernels' own times)
     prof_steps = max(2, min(args.steps, 5))

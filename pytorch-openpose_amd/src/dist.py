@@ -43,9 +43,11 @@ def gather_records(rec: torch.Tensor, n_frames: int, world: int, group=None) -> 
         out = torch.empty((world * cap, rb), dtype=rec.dtype, device=rec.device)
         dist.all_gather_into_tensor(out, rec.contiguous(), group=group)
         parts = list(out.view(world, cap, rb))
-    else:
-        parts = [torch.empty_like(rec) for _ in range(world)]
-        dist.all_gather(parts, rec.contiguous(), group=group)
+    else:  # gloo: through host memory
+        host = rec.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host.contiguous(), group=group)
+        parts = [p.to(rec.device) for p in parts]
     return torch.cat([p[:hi - lo] for p, (lo, hi) in zip(parts, per)], 0)
 
 
