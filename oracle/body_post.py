@@ -19,7 +19,6 @@ bit-exactly against the imported reference by tests/test_oracle_golden.py).
 """
 from __future__ import annotations
 
-import math
 
 import numpy as np
 from scipy.ndimage import gaussian_filter
@@ -212,7 +211,3 @@ def body_infer(ori: np.ndarray, net_fn, scale_search=(0.5,), boxsize=368, stride
         paf, heat = net_fn(x)
         lowres.append((np.asarray(paf)[0], np.asarray(heat)[0], pad, padded_hw))
     return post_from_lowres(ori.shape[:2], lowres, thre1, thre2, stride)
-
-
-def _unused():  # keep math imported for readers comparing with src/body.py:123
-    return math.sqrt

@@ -170,9 +170,9 @@ def gen_body_e2e():
         print("wrote", name, cand.shape, subset.shape)
 
 
-def gen_hand_planted():
+def gen_hand_planted(cases=((600, 96, 0.9, 0), (601, 150, 0.7, 2), (602, 64, 0.0, 0), (603, 200, 1.0, 3))):
     rng0 = np.random.default_rng(77)
-    for seed, size, vis_p, extra in ((600, 96, 0.9, 0), (601, 150, 0.7, 2), (602, 64, 0.0, 0), (603, 200, 1.0, 3)):
+    for seed, size, vis_p, extra in cases:
         rng = np.random.default_rng(seed)
         pts = rng0.uniform(0.15, 0.85, size=(21, 2))
         vis = rng.random(21) < vis_p
@@ -363,3 +363,109 @@ if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "batch":
     torch.set_num_threads(8)
     gen_batch_body()
     gen_batch_hand()
+
+
+# ---------------------------------------------------------------- C5: 1080p four-scale pyramid
+C5_SCALES = [0.5, 1.0, 1.5, 2.0]
+
+
+def ref_body_scales(model, scales):
+    """The reference's Body.__call__ with its commented-out multi-scale line active
+    (src/body.py:25-26): the method's own source, one assignment changed, compiled in the
+    reference module's namespace (nothing is written anywhere)."""
+    import inspect
+    import textwrap
+    import src.body as rb
+    code = textwrap.dedent(inspect.getsource(rb.Body.__call__))
+    old = "    scale_search = [0.5]\n"
+    assert code.count(old) == 1
+    code = code.replace(old, f"    scale_search = {list(scales)!r}\n")
+    ns = dict(vars(rb))
+    exec(compile(code, rb.__file__, "exec"), ns)
+    b = ref_body(model)
+    b.__class__ = type("BodyScales", (rb.Body,), {"__call__": ns["__call__"]})
+    return b
+
+
+class PlantedBodyScales:
+    """Stand-in network returning each scale's planted low-res maps, selected by input size."""
+
+    def __init__(self, by_shape):
+        self.by_shape = by_shape
+
+    def __call__(self, data):
+        paf, heat = self.by_shape[(data.shape[2] // 8, data.shape[3] // 8)]
+        return torch.from_numpy(paf[None]), torch.from_numpy(heat[None])
+
+
+def gen_body_c5():
+    """Planted 1080x1920 frame at scale_search = [0.5, 1, 1.5, 2] (BASELINE.json C5): the same
+    people rendered at every scale's low-res grid, the reference's multi-scale Body on them."""
+    from oracle.body_post import preprocess
+    H, W = 1080, 1920
+    for seed, n_people in ((700, 8), (701, 3)):
+        rng = np.random.default_rng(seed)
+        geo = []
+        for s in C5_SCALES:
+            _, pad, padded = preprocess(np.zeros((H, W, 3), np.uint8), s * 368 / H)
+            geo.append((padded[0] // 8, padded[1] // 8, pad, padded))
+        hl, wl = geo[-1][0], geo[-1][1]
+        people, vis = planted.random_people(rng, n_people, hl, wl, min_h=0.3, max_h=0.7)
+        maps, by_shape = {}, {}
+        for i, (h, w, pad, padded) in enumerate(geo):
+            # the 2.0-scale people mapped onto this scale's grid (pixel centres)
+            sy, sx = h / hl, w / wl
+            pts = (people + 0.5) * np.array([sx, sy]) - 0.5
+            paf, heat = planted.render_body(h, w, pts, vis, np.random.default_rng(seed * 10 + i),
+                                            sigma=0.9 * max(sy, 0.5), band=0.9 * max(sy, 0.6), noise=0.0)
+            by_shape[(h, w)] = (paf, heat)
+            maps[f"paf{i}"], maps[f"heat{i}"] = paf, heat
+            maps[f"pad{i}"], maps[f"padded{i}"] = np.array(pad), np.array(padded)
+        body = ref_body_scales(PlantedBodyScales(by_shape), C5_SCALES)
+        cand, subset = body(np.zeros((H, W, 3), np.uint8))
+        name = f"body_c5_{seed}_{H}x{W}_p{n_people}.npz"
+        np.savez_compressed(os.path.join(OUT, name), img_hw=np.array([H, W]), scales=np.array(C5_SCALES),
+                            candidate=cand, subset=subset, **maps)
+        print("wrote", name, "cand", cand.shape, "subset", subset.shape)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "c5":
+    install_shims()
+    sys.path.insert(0, REF)
+    torch.set_num_threads(8)
+    gen_body_c5()
+
+
+# ---------------------------------------------------------------- Body+Hand frame-pipeline glue
+def gen_glue():
+    """The reference's MotionData_every_frame (srcmx/MotionEstimation.py:126-216) with planted
+    Body / Hand stand-ins (oracle/glue_standins.py) in place of its module-level estimators."""
+    install_batch_shims()
+    from oracle import glue_standins as gs
+    import src.body
+    import src.hand
+    src.body.Body, src.hand.Hand = gs.StandInBody, gs.StandInHand
+    import MotionEstimation as me
+    assert isinstance(me.body_estimation, gs.StandInBody) and isinstance(me.hand_estimation, gs.StandInHand)
+    out = {}
+    for seed, H, W in gs.SCENES:
+        img = gs.frame(seed, H, W)
+        cand, subset = gs.scene(seed, H, W)
+        gs.StandInBody.register(img, cand, subset)
+        for mode in ("body", "bodyhand"):
+            out[f"pose_{seed}_{mode}"] = me.MotionData_every_frame(img, mode=mode)
+    np.savez_compressed(os.path.join(OUT, "glue_motion_every_frame.npz"),
+                        scenes=np.array(gs.SCENES), **out)
+    print("wrote glue_motion_every_frame.npz", {k: v.shape for k, v in out.items()})
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "glue":
+    sys.path.insert(0, REF)
+    gen_glue()
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "hand368":
+    # C3's crop size (BASELINE.json: per-detected-hand 368x368 crops)
+    install_shims()
+    sys.path.insert(0, REF)
+    gen_hand_planted(((604, 368, 0.85, 2),))

@@ -154,3 +154,34 @@ def test_scale_sharded_two_ranks_equals_single():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+# ---------------------------------------------------------------- C5 at its real size
+@pytest.mark.parametrize("name", ["body_c5_700_1080x1920_p8.npz", "body_c5_701_1080x1920_p3.npz"])
+def test_post_scales_c5_reference_golden(body, name):
+    """C5 (BASELINE.json): 1080x1920 at scale_search [0.5, 1, 1.5, 2]; planted per-scale maps,
+    expected output from the reference's own multi-scale Body (oracle/gen_golden.py c5):
+    bit-exact, host and device inputs."""
+    from conftest import GOLDEN
+    d = np.load(os.path.join(GOLDEN, name))
+    H, W = (int(v) for v in d["img_hw"])
+    assert tuple(d["scales"]) == SCALES
+    maps = [np.concatenate([d[f"paf{i}"], d[f"heat{i}"]], 0)[None] for i in range(len(SCALES))]
+    geo = body.scale_geom(H, W)
+    for i, (hl, wl, pd, pr) in enumerate(geo):
+        assert maps[i].shape[2:] == (hl, wl) and [pd, pr] == list(d[f"pad{i}"][2:])
+    cand, subset = body.post_scales(maps, H, W)[0]
+    assert np.array_equal(cand, d["candidate"]) and np.array_equal(subset, d["subset"])
+    dev = body.post_scales([torch.from_numpy(m).cuda() for m in maps], H, W)[0]
+    assert np.array_equal(dev[0], d["candidate"]) and np.array_equal(dev[1], d["subset"])
+
+
+def test_body_1080p_full_network_equals_scale_decomposition(body):
+    """One 1080p frame through the whole four-scale network: completes (status 0) and equals the
+    per-scale split that body_scale_sharded distributes (scale_maps per scale + post_scales)."""
+    img = np.random.default_rng(31).integers(0, 256, (1080, 1920, 3), dtype=np.uint8)
+    whole = body.batch(img[None])
+    cand, subset = whole[0]
+    assert cand.ndim == 2 and cand.shape[1] == 4 and subset.shape[1] == 20
+    maps = [body.scale_maps(img[None], s) for s in range(len(SCALES))]
+    _identical(body.post_scales(maps, 1080, 1920), whole)

@@ -48,6 +48,20 @@ def test_body_post_matches_reference(path):
     assert np.array_equal(subset, d["subset"])
 
 
+def _c5_lowres(d):
+    n = len(d["scales"])
+    return [(d[f"paf{i}"], d[f"heat{i}"], list(d[f"pad{i}"]), tuple(d[f"padded{i}"])) for i in range(n)]
+
+
+def test_body_post_c5_matches_reference():
+    """C5 (BASELINE.json): 1080x1920, scale_search [0.5, 1, 1.5, 2], the reference's multi-scale
+    Body on planted per-scale maps (oracle/gen_golden.py c5).  The 3-person case only here (the
+    float64 full-resolution NumPy path takes ~20 s); the GPU test covers both."""
+    d = np.load(os.path.join(GOLDEN, "body_c5_701_1080x1920_p3.npz"))
+    cand, subset = body_post.post_from_lowres(tuple(d["img_hw"]), _c5_lowres(d))
+    assert np.array_equal(cand, d["candidate"]) and np.array_equal(subset, d["subset"])
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("path", _files("body_e2e_*.npz"), ids=os.path.basename)
 def test_body_end_to_end_matches_reference(path):
