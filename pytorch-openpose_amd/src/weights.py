@@ -29,6 +29,16 @@ BENCH_OUT_SCALE = {
 }
 
 
+def c5_out_scale(heat_shift: float = -3.5, paf_offset: float = 0.8, heat_gain: float = 1.0) -> dict:
+    """BENCH_OUT_SCALE re-aimed at C5 (1080p, scale_search [0.5, 1, 1.5, 2]): the 368x656 heat
+    calibration carpets some channels of the averaged 1080p maps with plateau peaks, so the heat
+    pre-activations z become heat_gain * z + heat_shift (scripts/calib_c5.py picks them on the
+    GPU)."""
+    w, b = BENCH_OUT_SCALE["Mconv7_stage6_L2"]
+    return {"Mconv7_stage6_L2": ([v * heat_gain for v in w], [v * heat_gain + heat_shift for v in b]),
+            "Mconv7_stage6_L1": (1.0, paf_offset)}
+
+
 def seeded_state_dict(net: str = "body", seed: int = 0, out_scale: dict | None = None, as_torch: bool = False):
     rng = np.random.default_rng(seed)
     sd = OrderedDict()

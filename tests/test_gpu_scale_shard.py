@@ -176,9 +176,13 @@ def test_post_scales_c5_reference_golden(body, name):
     assert np.array_equal(dev[0], d["candidate"]) and np.array_equal(dev[1], d["subset"])
 
 
-def test_body_1080p_full_network_equals_scale_decomposition(body):
-    """One 1080p frame through the whole four-scale network: completes (status 0) and equals the
-    per-scale split that body_scale_sharded distributes (scale_maps per scale + post_scales)."""
+def test_body_1080p_full_network_equals_scale_decomposition():
+    """One 1080p frame through the whole four-scale network (C5 calibration of the seeded output
+    convs, as scripts/bench_configs.py runs it): completes (status 0) and equals the per-scale
+    split that body_scale_sharded distributes (scale_maps per scale + post_scales)."""
+    from src.body import Body
+    from src.weights import c5_out_scale, seeded_state_dict
+    body = Body(seeded_state_dict("body", 0, out_scale=c5_out_scale()), scale_search=SCALES)
     img = np.random.default_rng(31).integers(0, 256, (1080, 1920, 3), dtype=np.uint8)
     whole = body.batch(img[None])
     cand, subset = whole[0]
