@@ -29,14 +29,21 @@ BENCH_OUT_SCALE = {
 }
 
 
-def c5_out_scale(heat_shift: float = -3.5, paf_offset: float = 0.8, heat_gain: float = 1.0) -> dict:
-    """BENCH_OUT_SCALE re-aimed at C5 (1080p, scale_search [0.5, 1, 1.5, 2]): the 368x656 heat
-    calibration carpets some channels of the averaged 1080p maps with plateau peaks, so the heat
-    pre-activations z become heat_gain * z + heat_shift (scripts/calib_c5.py picks them on the
-    GPU)."""
-    w, b = BENCH_OUT_SCALE["Mconv7_stage6_L2"]
-    return {"Mconv7_stage6_L2": ([v * heat_gain for v in w], [v * heat_gain + heat_shift for v in b]),
-            "Mconv7_stage6_L1": (1.0, paf_offset)}
+# C5 (1080p, scale_search [0.5, 1, 1.5, 2]): the 368x656 calibration leaves most heat channels of
+# the averaged 1080p maps empty, so the heat conv gets its own per-channel affine, measured on
+# 1080p frames over the four scales' maps (scripts/calib_c5_stats.py: the 99.7th percentile of
+# each channel's pre-activations -> 0, its max -> 1; scripts/calib_c5_try.py: ~190 peaks and
+# ~10 assembled people per frame).  PAF as BENCH_OUT_SCALE.
+C5_OUT_SCALE = {
+    "Mconv7_stage6_L2": (
+        [6.799, 6.869, 4.388, 1.824, 4.797, 6.222, 4.417, 3.631, 5.173, 2.862, 2.307, 3.628, 5.313, 3.598, 3.523, 6.004, 4.872, 3.888, 2.677],
+        [-8.361, -6.269, 0.551, -2.099, -1.307, -7.711, -4.217, -1.382, -7.498, -2.706, 0.151, -2.059, 0.503, -7.834, -4.97, -1.486, -0.688, -4.525, 1.209]),
+    "Mconv7_stage6_L1": (1.0, 0.8),
+}
+
+
+def c5_out_scale() -> dict:
+    return C5_OUT_SCALE
 
 
 def seeded_state_dict(net: str = "body", seed: int = 0, out_scale: dict | None = None, as_torch: bool = False):
