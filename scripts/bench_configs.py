@@ -11,7 +11,6 @@ C5  1920x1080 frames with scale_search [0.5, 1.0, 1.5, 2.0] (averaged heat maps)
 """
 from __future__ import annotations
 
-import copy
 import json
 import os
 import sys
