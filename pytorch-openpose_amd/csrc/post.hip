@@ -37,7 +37,8 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
     return i < n ? i : p - 1 - i;
 }
 
-// Gaussian tile: TW x TH outputs of one map (+ the 1-pixel NMS ring).  scipy order: axis 0
+// Gaussian tile (the hand threshold, gauss_threshold; the body NMS uses the wide tile below):
+// TW x TH outputs of one map (+ the 1-pixel NMS ring).  scipy order: axis 0
 // (vertical) then axis 1, symmetric taps summed centre-first then |j| = 12 .. 1, float64, no FMA.
 //  * vertical pass straight from global memory: a thread owns one column of the tile's
 //    13-pixel-haloed footprint and half its rows, sliding a 41-entry register window down the
@@ -129,29 +130,116 @@ __device__ __forceinline__ void gauss_tile_coords(int H, int W, int& x0, int& y0
     gauss_tile_coords_of(H, W, gridDim.x, blockIdx.x, x0, y0, np);
 }
 
-// avg: [N*P][H][W] (float32 single scale / float64 average); one workgroup per tile.
-// `tiles` = all tiles; a grid smaller than that loops over them (grid-strided, a multiple of 8 so
-// every workgroup stays on its XCD's contiguous tile range): a capped grid leaves CUs to the
-// pipelined network's large-LDS conv workgroups
+// ---------------------------------------------------------------- Gaussian NMS (body peaks)
+// avg: [N*P][H][W] (float32 single scale / float64 average); one workgroup per tile of 102 x 30
+// outputs, so that both passes keep all 256 threads busy and the halo costs 2.43 filter
+// evaluations per output pixel (2.59 for gauss_tile's 64 x 32; 0.42 vs 1.15 ms per bench step):
+//  * vertical pass: thread = (column c of the 128-column footprint, half h of the 32 smoothed
+//    rows), a 40-entry float64 register window sliding down the column straight from global
+//    memory (coalesced rows); interior tiles step a pointer, border tiles reflect without
+//    divisions whenever the footprint lies within one reflection of the map (every tile of any
+//    map of at least 115 x 43);
+//  * horizontal pass: thread = (row r, 13-column run): its 37 inputs into registers, a barrier,
+//    then the 13 outputs written in place over the row (one LDS plane: 33 KB, 4 workgroups/CU);
+//    row stride 129 doubles: the 32 rows of a lane group fall in distinct bank pairs;
+//  * 4-neighbour NMS on the smoothed tile, then the reference's `> thre` (src/body.py:70-94).
+// scipy order throughout (axis 0 then axis 1; centre tap, then |j| = 12 .. 1 pairs), float64,
+// no FMA: bit-exact with scipy.ndimage.gaussian_filter(sigma=3).
+constexpr int WTW = 102, WTH = 30;      // outputs per tile
+constexpr int WVW = WTW + 26;           // 128 footprint / vertical-pass columns
+constexpr int WVR = WTH + 2;            // 32 smoothed rows incl. the NMS ring
+constexpr int WVH = WVR / 2;            // 16 rows per vertical thread
+constexpr int WGW = WTW + 2;            // 104 smoothed columns incl. the ring
+constexpr int WHC = WGW / 8;            // 13 columns per horizontal thread (8 runs x 32 rows)
+static_assert(WVW * 2 == 256 && WVR * 8 == 256 && WHC * 8 == WGW, "wide Gaussian tile");
+
+__device__ __forceinline__ int reflect_near(int i, int n) {  // valid for -n <= i < 2n
+    return i < 0 ? -1 - i : (i >= n ? 2 * n - 1 - i : i);
+}
+
+// MODE 0: footprint inside the map (no reflection: one pointer step per row); 1: within one
+// reflection of it (no divisions); 2: anything else (periodic reflect_idx)
+template <typename T, int MODE>
+__device__ __forceinline__ void gauss_wide_load(const T* __restrict__ m, int H, int W, int x0, int y0, int c, int h,
+                                                double (&win)[WVH + 24]) {
+    const int xi = x0 - 13 + c, r0 = y0 - 13 + h * WVH;
+    if constexpr (MODE == 0) {
+        const T* p = m + (size_t)r0 * W + xi;
+#pragma unroll
+        for (int i = 0; i < WVH + 24; ++i, p += W) win[i] = (double)*p;
+    } else {
+        const T* col = m + (MODE == 1 ? reflect_near(xi, W) : reflect_idx(xi, W));
+#pragma unroll
+        for (int i = 0; i < WVH + 24; ++i) {
+            const int ry = MODE == 1 ? reflect_near(r0 + i, H) : reflect_idx(r0 + i, H);
+            win[i] = (double)col[(size_t)ry * W];
+        }
+    }
+}
+
 template <typename T>
-__global__ __launch_bounds__(256) void gauss_nms(const T* __restrict__ avg, int tiles, int H, int W, double thre,
-                                                 int cap, int* __restrict__ cnt, int* __restrict__ list,
-                                                 double* __restrict__ list_score) {
-    __shared__ GaussTile t;
-    for (int b = blockIdx.x; b < tiles; b += gridDim.x) {
+__global__ __launch_bounds__(256) void gauss_nms_wide(const T* __restrict__ avg, int H, int W, double thre, int cap,
+                                                      int* __restrict__ cnt, int* __restrict__ list,
+                                                      double* __restrict__ list_score) {
+    __shared__ double sv[WVR][WVW + 1];
     int x0, y0, np;
-    gauss_tile_coords_of(H, W, tiles, b, x0, y0, np);
+    {
+        const int ntx = (W + WTW - 1) / WTW, nty = (H + WTH - 1) / WTH;
+        const int total = gridDim.x, b = blockIdx.x;
+        const int q = total >> 3, rr = total & 7, xcd = b & 7;
+        const int id = xcd * q + min(xcd, rr) + (b >> 3);  // XCD-contiguous tile ranges (guide T1)
+        const int tx = id % ntx, rest = id / ntx;
+        x0 = tx * WTW;
+        y0 = (rest % nty) * WTH;
+        np = rest / nty;
+    }
     const T* m = avg + (size_t)np * H * W;
-    if (gauss_tile(m, H, W, x0, y0, t, gauss_skip_below(thre))) {  // else no pixel can pass `> thre`
-    for (int e = threadIdx.x; e < TW * TH; e += 256) {
-        const int r = e / TW, c = e - r * TW;
-        const int y = y0 + r, x = x0 + c;
+    const int tid = threadIdx.x;
+    const int c = tid & (WVW - 1), h = tid >> 7;
+    double win[WVH + 24];
+    if (x0 >= 13 && x0 + WTW + 13 <= W && y0 >= 13 && y0 + WTH + 13 <= H)
+        gauss_wide_load<T, 0>(m, H, W, x0, y0, c, h, win);
+    else if (x0 - 13 >= -W && x0 + WTW + 13 <= 2 * W && y0 - 13 >= -H && y0 + WTH + 13 <= 2 * H)
+        gauss_wide_load<T, 1>(m, H, W, x0, y0, c, h, win);
+    else
+        gauss_wide_load<T, 2>(m, H, W, x0, y0, c, h, win);
+    bool hot = false;
+    const double skip_below = gauss_skip_below(thre);
+#pragma unroll
+    for (int i = 0; i < WVH + 24; ++i) hot |= win[i] >= skip_below;
+    if (!__syncthreads_or(hot)) return;  // no smoothed value can pass `> thre` (see gauss_tile)
+#pragma unroll
+    for (int i = 0; i < WVH; ++i) {
+        double acc = win[i + 12] * kGauss[0];
+#pragma unroll
+        for (int j = 12; j >= 1; --j) acc = acc + (win[i + 12 - j] + win[i + 12 + j]) * kGauss[j];
+        sv[h * WVH + i][c] = acc;
+    }
+    __syncthreads();
+    {
+        const int r = tid & (WVR - 1), c0 = (tid >> 5) * WHC;
+        double hw[WHC + 24];
+#pragma unroll
+        for (int i = 0; i < WHC + 24; ++i) hw[i] = sv[r][c0 + i];
+        __syncthreads();  // every thread holds its inputs: outputs go in place
+#pragma unroll
+        for (int i = 0; i < WHC; ++i) {
+            double acc = hw[i + 12] * kGauss[0];
+#pragma unroll
+            for (int j = 12; j >= 1; --j) acc = acc + (hw[i + 12 - j] + hw[i + 12 + j]) * kGauss[j];
+            sv[r][c0 + i] = acc;
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < WTW * WTH; e += 256) {
+        const int r = e / WTW, cc = e - r * WTW;
+        const int y = y0 + r, x = x0 + cc;
         if (y >= H || x >= W) continue;
-        const double v = t.g[r + 1][c + 1];
-        const double up = y > 0 ? t.g[r][c + 1] : 0.0;
-        const double dn = y < H - 1 ? t.g[r + 2][c + 1] : 0.0;
-        const double lf = x > 0 ? t.g[r + 1][c] : 0.0;
-        const double rt = x < W - 1 ? t.g[r + 1][c + 2] : 0.0;
+        const double v = sv[r + 1][cc + 1];
+        const double up = y > 0 ? sv[r][cc + 1] : 0.0;
+        const double dn = y < H - 1 ? sv[r + 2][cc + 1] : 0.0;
+        const double lf = x > 0 ? sv[r + 1][cc] : 0.0;
+        const double rt = x < W - 1 ? sv[r + 1][cc + 2] : 0.0;
         if (v >= up && v >= dn && v >= lf && v >= rt && v > thre) {
             const int slot = atomicAdd(cnt + np, 1);
             if (slot < cap) {
@@ -159,239 +247,6 @@ __global__ __launch_bounds__(256) void gauss_nms(const T* __restrict__ avg, int 
                 list_score[(size_t)np * cap + slot] = (double)m[(size_t)y * W + x];  // map_ori[y, x]
             }
         }
-    }
-    }
-    __syncthreads();  // t is refilled by the next tile
-    }
-}
-
-// ---------------------------------------------------------------- Gaussian NMS, screened
-// The same result as gauss_nms with most of the float64 work replaced by a float32 screen:
-//  1. the tile's input footprint (reflect-indexed, 58 x 90) goes to LDS; X = max |input|;
-//  2. the separable filter in float32 -> g32 for the tile + ring.  |g32 - g64| <= 56 * 2^-24 * X
-//     (two 25-tap passes, weights summing to 1, fp32 inputs / weights / sums), so with
-//     d = 1e-5 X + 1e-37 (> 2.6x that bound) every true peak (g64 > thre, g64 >= its 4
-//     neighbours) satisfies g32 > thre - d and g32 >= neighbour - 2d: a candidate;
-//  3. each candidate is re-evaluated exactly -- g64 at the pixel and its 4 neighbours from the
-//     LDS footprint in scipy's order (the 77 vertical sums they need, then 5 horizontal ones),
-//     one wave per candidate -- and the reference's test decides (src/body.py:70-94).
-// Non-finite inputs make d infinite: every pixel becomes a candidate (exact, slow path).
-// No LDS atomics and no wave-private LDS exchange: the candidate set stays as the ballot masks
-// of the screen pass (raster order, dealt round-robin to the 4 waves), X as one slot per wave,
-// and each round of 4 exact evaluations is bracketed by workgroup barriers.
-constexpr int GF_IR = VR + 24;        // footprint rows
-constexpr int GF_IT = TW * TH / 256;  // screen-pass iterations per thread
-struct GaussFastTile {
-    float v32[VR][VW];
-    float g32[VR][GW];
-    double vx[4][80];                   // exact vertical sums of each wave's candidate
-    unsigned long long mask[GF_IT][4];  // candidate ballots [iteration][wave]
-    float xmax[4];                      // per-wave max |input|
-};
-
-template <typename T>
-__global__ __launch_bounds__(256) void gauss_nms_screened(const T* __restrict__ avg, int P, int H, int W,
-                                                          double thre, int cap, int* __restrict__ cnt,
-                                                          int* __restrict__ list, double* __restrict__ list_score) {
-    __shared__ GaussFastTile t;
-    __shared__ T s_in[GF_IR][VW];
-    int x0, y0, np;
-    gauss_tile_coords(H, W, x0, y0, np);
-    const T* m = avg + (size_t)np * H * W;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const double skip_below = gauss_skip_below(thre);
-    // 1. footprint -> registers (vertical threads: column c, half h) and LDS; skip test; X
-    bool hot = false;
-    float amax = 0.f;
-    const bool vt = tid < 2 * VW;
-    const int c = tid % VW, h = tid / VW;
-    double win[VH + 24];
-    if (vt) {
-        const T* col = m + reflect_idx(x0 - 13 + c, W);
-        const int r0 = y0 - 13 + h * VH;
-#pragma unroll
-        for (int i = 0; i < VH + 24; ++i) win[i] = (double)col[(size_t)reflect_idx(r0 + i, H) * W];
-#pragma unroll
-        for (int i = 0; i < VH + 24; ++i) {
-            hot |= win[i] >= skip_below;
-            amax = fmaxf(amax, fabsf((float)win[i]));  // NaN ignored; inf -> inf
-            if (h == 0 || i >= 24) s_in[h * VH + i][c] = (T)win[i];
-        }
-    }
-    if (!__syncthreads_or(hot)) return;  // no pixel can pass `> thre` (see gauss_tile)
-    for (int off = 32; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
-    if (lane == 0) t.xmax[wave] = amax;
-    // 2a. float32 vertical pass
-    float w32[13];
-#pragma unroll
-    for (int j = 0; j < 13; ++j) w32[j] = (float)kGauss[j];
-    if (vt) {
-#pragma unroll
-        for (int i = 0; i < VH; ++i) {
-            float acc = (float)win[i + 12] * w32[0];
-#pragma unroll
-            for (int j = 12; j >= 1; --j) acc = acc + ((float)win[i + 12 - j] + (float)win[i + 12 + j]) * w32[j];
-            t.v32[h * VH + i][c] = acc;
-        }
-    }
-    __syncthreads();
-    // 2b. float32 horizontal pass
-    if (tid < VR * 7) {
-        const int r = tid % VR, c0 = (tid / VR) * HC;
-        float fw[HC + 24];
-#pragma unroll
-        for (int i = 0; i < HC + 24; ++i) fw[i] = (c0 + i < VW) ? t.v32[r][c0 + i] : 0.f;
-#pragma unroll
-        for (int i = 0; i < HC; ++i) {
-            if (c0 + i < GW) {
-                float acc = fw[i + 12] * w32[0];
-#pragma unroll
-                for (int j = 12; j >= 1; --j) acc = acc + (fw[i + 12 - j] + fw[i + 12 + j]) * w32[j];
-                t.g32[r][c0 + i] = acc;
-            }
-        }
-    }
-    __syncthreads();
-    // 2c. candidates
-    const float X = fmaxf(fmaxf(t.xmax[0], t.xmax[1]), fmaxf(t.xmax[2], t.xmax[3]));
-    const double d = isfinite(X) ? 1e-5 * (double)X + 1e-37 : INFINITY;
-#pragma unroll
-    for (int k = 0; k < GF_IT; ++k) {
-        const int e = tid + 256 * k;
-        const int r = e / TW, cc = e - r * TW;
-        const int y = y0 + r, x = x0 + cc;
-        bool cand = false;
-        if (y < H && x < W) {
-            const double v = t.g32[r + 1][cc + 1];
-            const double up = y > 0 ? (double)t.g32[r][cc + 1] : 0.0;
-            const double dn = y < H - 1 ? (double)t.g32[r + 2][cc + 1] : 0.0;
-            const double lf = x > 0 ? (double)t.g32[r + 1][cc] : 0.0;
-            const double rt = x < W - 1 ? (double)t.g32[r + 1][cc + 2] : 0.0;
-            cand = (v > thre - d && v >= up - 2 * d && v >= dn - 2 * d && v >= lf - 2 * d && v >= rt - 2 * d) ||
-                   d == INFINITY;
-        }
-        const unsigned long long bal = __ballot(cand);
-        if (lane == 0) t.mask[k][wave] = bal;
-    }
-    __syncthreads();
-    // 3. exact evaluation: candidate i (raster order) goes to wave i % 4; every wave walks the
-    //    same masks, so the round count is uniform and each round sits between two barriers
-    int nc = 0;
-#pragma unroll
-    for (int k = 0; k < GF_IT; ++k)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) nc += (int)__popcll(t.mask[k][w]);
-    int ck = 0, cw = 0;
-    unsigned long long cm = t.mask[0][0];
-    double* vx = t.vx[wave];
-    for (int round = 0; round < (nc + 3) / 4; ++round) {
-        int e = -1;
-        for (int j = 0; j < 4; ++j) {  // advance the cursor by 4 candidates, keep the wave's one
-            while (cm == 0 && ck < GF_IT) {
-                if (++cw == 4) {
-                    cw = 0;
-                    ++ck;
-                }
-                cm = ck < GF_IT ? t.mask[ck][cw] : 0ull;
-            }
-            if (cm == 0) break;
-            const int b = __builtin_ctzll(cm);
-            cm &= cm - 1;
-            if (j == wave) e = ck * 256 + cw * 64 + b;
-        }
-        const int r = e / TW, cc = e - r * TW;
-        const int y = y0 + r, x = x0 + cc;
-        // vertical sums: idx < 27 -> v row r+1, cols cc..cc+26; < 52 -> row r, cols cc+1..;
-        // else row r+2, cols cc+1.. (v row R <-> footprint rows R .. R+24, image row y0-1+R)
-        if (e >= 0) {
-            for (int idx = lane; idx < 77; idx += 64) {
-                const int R = idx < 27 ? r + 1 : (idx < 52 ? r : r + 2);
-                const int C = idx < 27 ? cc + idx : (idx < 52 ? cc + 1 + (idx - 27) : cc + 1 + (idx - 52));
-                double acc = (double)s_in[R + 12][C] * kGauss[0];
-#pragma unroll
-                for (int j = 12; j >= 1; --j)
-                    acc = acc + ((double)s_in[R + 12 - j][C] + (double)s_in[R + 12 + j][C]) * kGauss[j];
-                vx[idx] = acc;
-            }
-        }
-        __syncthreads();
-        if (e >= 0) {
-            // horizontal sums: 0 centre, 1 left, 2 right, 3 up, 4 down (window base in vx)
-            double g = 0.0;
-            if (lane < 5) {
-                const int base = lane == 0 ? 1 : lane == 1 ? 0 : lane == 2 ? 2 : lane == 3 ? 27 : 52;
-                g = vx[base + 12] * kGauss[0];
-#pragma unroll
-                for (int j = 12; j >= 1; --j) g = g + (vx[base + 12 - j] + vx[base + 12 + j]) * kGauss[j];
-            }
-            const double v = __shfl(g, 0), lfv = __shfl(g, 1), rtv = __shfl(g, 2), upv = __shfl(g, 3),
-                         dnv = __shfl(g, 4);
-            const double up = y > 0 ? upv : 0.0;
-            const double dn = y < H - 1 ? dnv : 0.0;
-            const double lf = x > 0 ? lfv : 0.0;
-            const double rt = x < W - 1 ? rtv : 0.0;
-            if (lane == 0 && v >= up && v >= dn && v >= lf && v >= rt && v > thre) {
-                const int slot = atomicAdd(cnt + np, 1);
-                if (slot < cap) {
-                    list[(size_t)np * cap + slot] = y * W + x;
-                    list_score[(size_t)np * cap + slot] = (double)m[(size_t)y * W + x];  // map_ori[y, x]
-                }
-            }
-        }
-        __syncthreads();  // vx is rewritten in the next round
-    }
-}
-
-// Debug (OPOSE_GAUSS_DEBUG=1 with the screened kernel): the all-float64 kernel runs after it on the
-// same stream into shadow lists; one thread per map reports every peak of B missing from A with
-// the screen's float32 values at that pixel, recomputed in the screen's order.
-template <typename T>
-__global__ void gauss_debug_cmp(const T* __restrict__ avg, int NP, int H, int W, double thre, int cap,
-                                const int* cntA, const int* listA, const int* cntB, const int* listB) {
-    const int np = blockIdx.x * blockDim.x + threadIdx.x;
-    if (np >= NP) return;
-    const int na = min(cntA[np], cap), nb = min(cntB[np], cap);
-    const T* m = avg + (size_t)np * H * W;
-    for (int i = 0; i < nb; ++i) {
-        const int pb = listB[(size_t)np * cap + i];
-        bool found = false;
-        for (int j = 0; j < na; ++j) found |= listA[(size_t)np * cap + j] == pb;
-        if (found) continue;
-        const int y = pb / W, x = pb % W;
-        // footprint of the pixel's screened tile: max |input| (the screen's X)
-        const int x0 = (x / TW) * TW, y0 = (y / TH) * TH;
-        float X = 0.f;
-        for (int r = 0; r < GF_IR; ++r)
-            for (int c = 0; c < VW; ++c)
-                X = fmaxf(X, fabsf((float)m[(size_t)reflect_idx(y0 - 13 + r, H) * W + reflect_idx(x0 - 13 + c, W)]));
-        float w32[13];
-        for (int j = 0; j < 13; ++j) w32[j] = (float)kGauss[j];
-        float g[5];  // centre, up, down, left, right
-        const int dy[5] = {0, -1, 1, 0, 0}, dx[5] = {0, 0, 0, -1, 1};
-        for (int k = 0; k < 5; ++k) {
-            const int yy = y + dy[k], xx = x + dx[k];
-            float v[25];
-            for (int cc = 0; cc < 25; ++cc) {
-                const int col = reflect_idx(xx - 12 + cc, W);
-                float acc = (float)m[(size_t)reflect_idx(yy, H) * W + col] * w32[0];
-                for (int j = 12; j >= 1; --j)
-                    acc = acc + ((float)m[(size_t)reflect_idx(yy - j, H) * W + col] +
-                                 (float)m[(size_t)reflect_idx(yy + j, H) * W + col]) * w32[j];
-                v[cc] = acc;
-            }
-            float a = v[12] * w32[0];
-            for (int j = 12; j >= 1; --j) a = a + (v[12 - j] + v[12 + j]) * w32[j];
-            g[k] = a;
-        }
-        printf("GAUSSDBG map %d y %d x %d missing: cntA %d cntB %d  g32 %.9g up %.9g dn %.9g lf %.9g rt %.9g  X %.9g "
-               "thre %.9g in %.9g\n",
-               np, y, x, cntA[np], cntB[np], g[0], g[1], g[2], g[3], g[4], X, thre, (double)m[(size_t)y * W + x]);
-    }
-    for (int j = 0; j < na; ++j) {
-        const int pa = listA[(size_t)np * cap + j];
-        bool found = false;
-        for (int i = 0; i < nb; ++i) found |= listB[(size_t)np * cap + i] == pa;
-        if (!found) printf("GAUSSDBG map %d y %d x %d extra in screened\n", np, pa / W, pa % W);
     }
 }
 
@@ -862,66 +717,12 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
 // ------------------------------------------------------------------ launchers
 void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
                       double* list_score, hipStream_t st) {
-    dim3 grid(((W + TW - 1) / TW) * ((H + TH - 1) / TH) * NP);
-    // default: the all-float64 tile kernel.  OPOSE_GAUSS_SCREEN=1: float32 screen + exact
-    // re-evaluation.  Its overlap-only peak loss (round 1) was the compiler's packed-FP32 code in
-    // the float32 horizontal pass: wrong low-element sums when the launch shared the chip with the
-    // pipelined network stream, exact alone; the library is now built without packed FP32
-    // (Makefile NOPK).  OPOSE_GAUSS_DEBUG=1 runs the float64 kernel after it into
-    // shadow lists and prints every difference from the device (scripts/gauss_debug.sh).
-    static const bool screened = [] {
-        const char* e = getenv("OPOSE_GAUSS_SCREEN");
-        return e && e[0] == '1';
-    }();
-    if (screened) {
-        if (f32)
-            hipLaunchKernelGGL(gauss_nms_screened<float>, grid, dim3(256), 0, st, (const float*)avg, 18, H, W, thre,
-                               cap, cnt, list, list_score);
-        else
-            hipLaunchKernelGGL(gauss_nms_screened<double>, grid, dim3(256), 0, st, (const double*)avg, 18, H, W,
-                               thre, cap, cnt, list, list_score);
-        static const bool dbg = getenv("OPOSE_GAUSS_DEBUG") != nullptr;
-        if (dbg) {
-            static int* sh = nullptr;
-            static size_t sh_n = 0;
-            const size_t need = (size_t)NP * (cap + 1);
-            if (need > sh_n) {
-                OPOSE_HIP_CHECK(hipDeviceSynchronize());
-                if (sh) OPOSE_HIP_CHECK(hipFree(sh));
-                OPOSE_HIP_CHECK(hipMalloc(&sh, need * (4 + 8)));
-                sh_n = need;
-            }
-            int* c2 = sh;
-            int* l2 = sh + NP;
-            double* s2 = reinterpret_cast<double*>(sh + need + (need & 1));
-            OPOSE_HIP_CHECK(hipMemsetAsync(c2, 0, 4 * NP, st));
-            const int tiles = (int)grid.x;
-            if (f32) {
-                hipLaunchKernelGGL(gauss_nms<float>, grid, dim3(256), 0, st, (const float*)avg, tiles, H, W, thre, cap,
-                                   c2, l2, s2);
-                hipLaunchKernelGGL(gauss_debug_cmp<float>, dim3((NP + 63) / 64), dim3(64), 0, st, (const float*)avg,
-                                   NP, H, W, thre, cap, cnt, list, c2, l2);
-            } else {
-                hipLaunchKernelGGL(gauss_nms<double>, grid, dim3(256), 0, st, (const double*)avg, tiles, H, W, thre,
-                                   cap, c2, l2, s2);
-                hipLaunchKernelGGL(gauss_debug_cmp<double>, dim3((NP + 63) / 64), dim3(64), 0, st,
-                                   (const double*)avg, NP, H, W, thre, cap, cnt, list, c2, l2);
-            }
-        }
-        return;
-    }
-    // OPOSE_GAUSS_GRID=n (multiple of 8): at most n workgroups looping over the tiles
-    static const int gcap = [] {
-        const char* e = getenv("OPOSE_GAUSS_GRID");
-        return e ? (atoi(e) / 8) * 8 : 0;
-    }();
-    const int tiles = (int)grid.x;
-    const dim3 g2(gcap > 0 && gcap < tiles ? gcap : tiles);
+    const dim3 grid(((W + WTW - 1) / WTW) * ((H + WTH - 1) / WTH) * NP);
     if (f32)
-        hipLaunchKernelGGL(gauss_nms<float>, g2, dim3(256), 0, st, (const float*)avg, tiles, H, W, thre, cap, cnt,
+        hipLaunchKernelGGL(gauss_nms_wide<float>, grid, dim3(256), 0, st, (const float*)avg, H, W, thre, cap, cnt,
                            list, list_score);
     else
-        hipLaunchKernelGGL(gauss_nms<double>, g2, dim3(256), 0, st, (const double*)avg, tiles, H, W, thre, cap, cnt,
+        hipLaunchKernelGGL(gauss_nms_wide<double>, grid, dim3(256), 0, st, (const double*)avg, H, W, thre, cap, cnt,
                            list, list_score);
 }
 

@@ -1,5 +1,4 @@
-"""GPU: the Gaussian NMS stage (csrc/post.hip gauss_nms; with OPOSE_GAUSS_SCREEN=1 the opt-in
-gauss_nms_screened, float32 screen + exact float64 re-evaluation) against the oracle's scipy
+"""GPU: the Gaussian NMS stage (csrc/post.hip gauss_nms_wide) against the oracle's scipy
 gaussian_filter + 4-neighbour NMS (src/body.py:70-94) on maps built to stress float64
 near-ties: flat plateaus (neighbours within float32 noise of each other), dense noise (many
 local maxima), values hugging the threshold, a single-pixel spike, and the two-scale float64
@@ -68,4 +67,19 @@ def test_screened_nms_two_scales_float64_average():
         maps.append(np.concatenate([paf, heat], 0)[None])
     cand, subset = body2.post_scales(maps, H, W)[0]
     ref_c, ref_s = body_post.post_from_lowres((H, W), lowres)
+    assert np.array_equal(cand, ref_c) and np.array_equal(subset, ref_s)
+
+
+@pytest.mark.parametrize("hw", [(2, 5), (3, 14), (16, 2)], ids=lambda v: f"{v[0]}x{v[1]}")
+def test_nms_maps_smaller_than_one_reflection(body, hw):
+    """Maps so small that the 13-pixel filter footprint wraps more than once (scipy's periodic
+    reflect; the kernel's division-based index path)."""
+    hl, wl = hw
+    rng = np.random.default_rng(11 + hl)
+    heat = (rng.random((19, hl, wl), dtype=np.float32) * np.float32(0.9)).astype(np.float32)
+    paf = (rng.standard_normal((38, hl, wl)) * 0.3).astype(np.float32)
+    H, W = hl * 8, wl * 8
+    pad = [0, 0, 0, 0]
+    cand, subset = body.post(np.concatenate([paf, heat], 0)[None], pad, H, W)[0]
+    ref_c, ref_s = body_post.post_from_lowres((H, W), [(paf, heat, pad, (H, W))])
     assert np.array_equal(cand, ref_c) and np.array_equal(subset, ref_s)
