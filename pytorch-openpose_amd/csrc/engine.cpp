@@ -205,6 +205,14 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_FIRST_DIRECT");
         return !(e && e[0] == '0');
     }();
+    // conv1_1 + conv1_2 + pool in one launch (conv12_pool_x6; needs first_direct and fused_pool),
+    // opt-in (OPOSE_CONV12_FUSED=1): bit-identical, but 1.33 ms per bench step against 1.12 ms
+    // for the pooled conv1_2 plus a conv1_1 that overlaps the previous step's post kernels
+    // (conv_x6.hip)
+    bool fused12 = [] {
+        const char* e = getenv("OPOSE_CONV12_FUSED");
+        return e && e[0] == '1';
+    }();
     DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[2][kMaxScales], avg, cnt, list, peak_pos,
         part_cnt, score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score, skcnt, hsel;
     // Cross-call pipelining of opose_body_infer calls flagged OPOSE_PIPELINE (device input and
@@ -658,6 +666,28 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
     for (size_t i = 0; i < vgg.size(); ++i) {
         const Spec& s = vgg[i];
         DevConv* c = find_conv(h, net, s.name);
+        if (i == 0 && s.cin == 3 && s.cout == 64 && s.ks == 3 && s.pad == 1 && vgg.size() > 2 && h->first_direct &&
+            h->fused12 && h->fused_pool && vgg[1].name == "conv1_2" && H % 8 == 0 && W % 2 == 0) {
+            DevConv* c2 = find_conv(h, net, vgg[1].name);
+            if (c2->cin == 64 && c2->cout == 64 && c2->ks == 3 && c2->pad == 1 && c2->Mpad == 64 && c2->nK6 == 18 &&
+                !c2->small6 && c->Mpad >= 64) {
+                // conv1_1 -> conv1_2 -> MaxPool2d in one launch: the 64-channel full-resolution
+                // tensor between them never reaches HBM
+                const size_t npo = (size_t)N * (H / 2) * (W / 2);
+                ProfEntry pe;
+                h->prof_begin(pe, "conv3x3", 2.0 * 64 * (27 + 576) * (double)npix, 0);
+                if (h->detail) pe.detail = "layer/conv1_1+conv1_2+pool/fused/n" + std::to_string(npix);
+                launch_conv12_pool_x6(x, N, H, W, c->wt, c->Mpad, c->bias, c2->wx6, c2->bias, A,
+                                      (uint32_t)(npo * 8 * 16), h->stream);
+                h->prof_end(pe);
+                cur = A;
+                cg = 8;
+                hh = H / 2;
+                ww = W / 2;
+                ++i;  // conv1_2 (and its pool) done
+                continue;
+            }
+        }
         if (i == 0 && s.cin == 3 && s.cout == 64 && s.ks == 3 && s.pad == 1 && vgg.size() > 1 && h->first_direct) {
             // conv1_1 straight from the fp32 input (conv_first_x6), no input split
             ProfEntry pe;

@@ -151,3 +151,32 @@ def test_network_variants(native, env):
             tol = 2e-4 * np.abs(r).max() + 2e-4 * np.abs(r)
             assert (np.abs(a - r) <= tol).all(), kind
             assert np.abs(a - r).max() <= 1e-5 * np.abs(r).max(), kind
+
+
+def test_conv12_fused_bit_identical(native):
+    """conv1_1 + conv1_2 + MaxPool2d in one launch (conv12_pool_x6, opt-in OPOSE_CONV12_FUSED=1)
+    against the separate conv_first_x6 and pooled conv_x6 launches (default): the same fp32 FMA order for
+    conv1_1 and the same MFMA sequence per output, so the network outputs are bit-identical.
+    Shapes with a partial 16-column tile (104 / 88 columns) and several frames."""
+    from src import util
+    from src.model import bodypose_model, handpose_model
+    from src.weights import seeded_state_dict
+    for kind, cls, shape in (("body", bodypose_model, (2, 3, 72, 104)), ("hand", handpose_model, (1, 3, 88, 88))):
+        sd = seeded_state_dict(kind, 0)
+        x = np.random.default_rng(9).random(shape, dtype=np.float32) - np.float32(0.5)
+        outs = []
+        for on in ("1", "0"):
+            old = os.environ.get("OPOSE_CONV12_FUSED")
+            os.environ["OPOSE_CONV12_FUSED"] = on
+            try:
+                m = cls(0)
+            finally:
+                if old is None:
+                    del os.environ["OPOSE_CONV12_FUSED"]
+                else:
+                    os.environ["OPOSE_CONV12_FUSED"] = old
+            m.load_state_dict(util.transfer(m, sd))
+            y = m(x)
+            outs.append(y if isinstance(y, tuple) else (y,))
+        for a, r in zip(*outs):
+            assert np.array_equal(a, r), kind
