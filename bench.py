@@ -281,6 +281,41 @@ def host_to_host(body, frames_np, steps, dev, rank, world):
     return world * B * steps / dt, dt / steps * 1e3
 
 
+def hand_c3(device, iters):
+    """C3's Hand leg: Hand() (src/hand.py:25-75) on one 368x368 crop, 4 scales, host in -> host
+    out; per-stage times and the conv roofline from a profiled pass of the same calls."""
+    from src.hand import Hand
+    from src.weights import seeded_state_dict
+    hand = Hand(seeded_state_dict("hand", 0), device=device)
+    crop = np.random.default_rng(5).integers(0, 256, (368, 368, 3), dtype=np.uint8)
+    for _ in range(2):
+        hand(crop)
+    ts = []
+    for _ in range(iters):
+        t1 = time.perf_counter()
+        hand(crop)
+        ts.append(time.perf_counter() - t1)
+    ms = float(np.median(ts)) * 1e3
+    hand.handle.profile(1)
+    hand.handle.profile_reset()
+    for _ in range(3):
+        hand(crop)
+    prof = hand.handle.profile_read()
+    hand.handle.profile(False)
+    conv = {k: v for k, v in prof.items() if k.startswith("conv")}
+    flops = sum(v["flops"] for v in conv.values()) / 3
+    conv_ms = sum(v["ms"] for v in conv.values()) / 3
+    return {"workload": "C3 Hand(): one 368x368 crop, scale_search [0.5, 1, 1.5, 2], host in -> host out",
+            "latency_ms": ms, "conv_tflop_per_call": flops / 1e12,
+            "conv_ms_per_call": conv_ms,
+            "conv_roofline": {"bound": "mfma", "achieved": flops / (conv_ms * 1e-3) / 1e12 if conv_ms else None,
+                              "peak": PEAK_CONV_TFLOPS, "unit": "TFLOP/s",
+                              "frac": (flops / (conv_ms * 1e-3) / 1e12) / PEAK_CONV_TFLOPS if conv_ms else None},
+            "stage_ms_per_call": {k: round(v["ms"] / 3, 4) for k, v in sorted(prof.items())},
+            "stage_roofline": stage_roofline({k: dict(v, ms=v["ms"] / 3, flops=v["flops"] / 3, bytes=v["bytes"] / 3)
+                                              for k, v in prof.items()})}
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -378,6 +413,8 @@ def main():
     # host-to-host (PCIe-inclusive) pass: reported beside `value`, never as it
     h2h_value, h2h_ms = host_to_host(body, frames_np, args.host_steps or args.steps, dev, rank, world)
 
+    c3 = hand_c3(local, args.latency_iters) if rank == 0 and args.latency_iters > 0 else None
+
     # single-frame latency (C2: one frame, host in -> host out through Body.__call__)
     lat = []
     if rank == 0 and args.latency_iters > 0:
@@ -437,6 +474,7 @@ def main():
             "stage_ms_per_step": stage_ms,
             "stage_roofline": stage_roofline(prof),
             "latency_ms_single_frame": (float(np.median(lat)) * 1e3) if lat else None,
+            "c3_hand": c3,
             "frames_status_nonzero": int((statuses != 0).sum()),
             "mean_peaks_per_frame": float(counts[:, 0].mean()),
             "mean_people_per_frame": float(counts[:, 1].mean()),

@@ -54,3 +54,28 @@ def test_pipeline_body_mode_picks_rightmost_left_shoulder():
     for k in range(18):
         idx = int(sub[best][k])
         assert np.array_equal(pose[k], cand[idx][:3] if idx != -1 else np.zeros(3))
+
+
+def test_draw_bodypose_marks_keypoints_and_limbs():
+    """src/util.py:44-77 (OpenCV pixel parity unpinned: cv2 is absent): discs of the part colours
+    at every keypoint, blended limb ellipses between connected parts, nothing elsewhere."""
+    from src import util
+    canvas = np.zeros((120, 160, 3), np.uint8)
+    # one person: neck (1) at (80, 40), right shoulder (2) at (60, 40), right elbow (3) at (55, 70)
+    candidate = np.array([[80.0, 40.0, 0.9, 0], [60.0, 40.0, 0.8, 1], [55.0, 70.0, 0.7, 2]])
+    subset = -1 * np.ones((1, 20))
+    subset[0, 1], subset[0, 2], subset[0, 3] = 0, 1, 2
+    out = util.draw_bodypose(canvas, candidate, subset)
+    assert out.shape == canvas.shape and out.dtype == np.uint8
+    assert tuple(canvas[40, 80]) == (255, 85, 0)  # the neck disc (part 1 colour), drawn in place (as cv2.circle)
+    assert out[40, 70].any()  # the neck-shoulder limb between them
+    assert not out[110, 150].any() and not out[5, 5].any()
+
+
+def test_draw_handpose_renders_rgb():
+    from src import util
+    canvas = np.zeros((60, 80, 3), np.uint8)
+    peaks = np.zeros((21, 2))
+    peaks[0], peaks[1], peaks[2] = (10, 10), (20, 15), (30, 25)
+    img = util.draw_handpose(canvas, [peaks])
+    assert img.ndim == 3 and img.shape[2] == 3 and img.dtype == np.uint8 and img.any()
