@@ -186,8 +186,6 @@ struct opose_ctx {
     std::map<std::string, std::unique_ptr<DevConv>> convs[2];
     bool loaded[2] = {false, false};
     // workspace
-    // split-bf16 (X6) activations of the x6 network path (conv_x6.hip)
-    DevBuf x6in, x6A, x6B, x6S0, x6S1, x6T0, x6T1, x6U;
     // network convolutions: fp32-accurate split-bf16 kernel (default) or the fp32 MFMA kernel
     // (OPOSE_CONV=f32)
     bool x6 = [] {
@@ -213,8 +211,24 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_CONV12_FUSED");
         return e && e[0] == '1';
     }();
-    DevBuf frames, x, bufA, bufB, S0, S1, T0, T1, U, partial, mids[2][kMaxScales], avg, cnt, list, peak_pos,
-        part_cnt, score, conn, conn_cnt, records, maps_in, hlab, hsums, hpeaks, hfound, list_score, skcnt, hsel;
+    DevBuf frames, mids[2][kMaxScales], avg, cnt, list, peak_pos, part_cnt, score, conn, conn_cnt, records, maps_in,
+        hlab, hsums, hpeaks, hfound, list_score, hsel;
+    // network workspace, one set per concurrently running scale (slot s runs on scale_stream(s);
+    // slot 0 is the handle's stream): input, activations, stream-K slabs
+    struct NetWS {
+        DevBuf x, x6in, x6A, x6B, x6S0, x6S1, x6T0, x6T1, x6U, bufA, bufB, S0, S1, T0, T1, U, partial, skcnt;
+    };
+    NetWS ws[kMaxScales];
+    int slot = 0;
+    NetWS& w() { return ws[slot]; }
+    // the scales of one Hand() call run concurrently on their own streams (OPOSE_SCALE_STREAMS=0:
+    // one after another on the handle's stream, captured into a hipGraph)
+    bool scale_streams = [] {
+        const char* e = getenv("OPOSE_SCALE_STREAMS");
+        return !(e && e[0] == '0');
+    }();
+    hipStream_t sstream[kMaxScales] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[kMaxScales] = {};
     // Cross-call pipelining of opose_body_infer calls flagged OPOSE_PIPELINE (device input and
     // output; OPOSE_PIPELINE=0 in the environment at handle creation: never).  Call k's network part (preprocess, conv stack,
     // x8 upsample) runs on `nstream`, its post-network part on `stream` after an event; call
@@ -247,9 +261,10 @@ struct opose_ctx {
     // workgroup resets its tile), zero-filled whenever the buffer grows
     int* sk_counters(int tiles) {
         if (sk_fixup_kernel) return nullptr;
-        const size_t before = skcnt.bytes;
-        int* c = skcnt.ensure<int>((size_t)tiles, stream);
-        if (skcnt.bytes != before) OPOSE_HIP_CHECK(hipMemsetAsync(c, 0, skcnt.bytes, stream));
+        DevBuf& sk = w().skcnt;
+        const size_t before = sk.bytes;
+        int* c = sk.ensure<int>((size_t)tiles, stream);
+        if (sk.bytes != before) OPOSE_HIP_CHECK(hipMemsetAsync(c, 0, sk.bytes, stream));
         return c;
     }
     // profiling
@@ -312,8 +327,15 @@ struct opose_ctx {
             (void)hipStreamSynchronize(nstream);
             (void)hipStreamDestroy(nstream);
         }
-        for (hipEvent_t e : {ev_net, ev_main, ev_post[0], ev_post[1], ev_ext, ev_sig})
+        for (hipEvent_t e : {ev_net, ev_main, ev_post[0], ev_post[1], ev_ext, ev_sig, ev_fork})
             if (e) (void)hipEventDestroy(e);
+        for (int i = 0; i < kMaxScales; ++i) {
+            if (sstream[i]) {
+                (void)hipStreamSynchronize(sstream[i]);
+                (void)hipStreamDestroy(sstream[i]);
+            }
+            if (ev_join[i]) (void)hipEventDestroy(ev_join[i]);
+        }
         for (auto& kv : graphs)
             if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
         for (auto e : event_pool) (void)hipEventDestroy(e);
@@ -530,7 +552,7 @@ static void run_conv(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W
     const TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.Kpad / 32);
     a.ngroups = ng;
     a.sk_grid = t.grid;
-    a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+    a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
     a.sk_cnt = h->sk_counters((a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * ng);
     double flops = 0;
     for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)a.K * a.npix;
@@ -554,8 +576,8 @@ static void run_pool(opose_ctx* h, const float* in, float* out, int NC, int H, i
 static void run_trunk(opose_ctx* h, int net, const float* x, int N, int H, int W, Act last, Act dup) {
     const std::vector<Spec> vgg = net == OPOSE_NET_BODY ? vgg_body() : vgg_hand();
     size_t act = (size_t)N * 64 * H * W;
-    float* A = h->bufA.ensure<float>(act, h->stream);
-    float* B = h->bufB.ensure<float>(act, h->stream);
+    float* A = h->w().bufA.ensure<float>(act, h->stream);
+    float* B = h->w().bufB.ensure<float>(act, h->stream);
     const float* cur = x;
     int cc = 3, hh = H, ww = W;
     for (size_t i = 0; i < vgg.size(); ++i) {
@@ -642,7 +664,7 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
     if (pool) t.grid = (a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * ng;  // whole tiles (data parallel)
     a.ngroups = ng;
     a.sk_grid = t.grid;
-    a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+    a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
     double flops = 0;
     for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)c0->K * a.npix;
     ProfEntry pe;
@@ -659,8 +681,8 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
     const std::vector<Spec> vgg = net == OPOSE_NET_BODY ? vgg_body() : vgg_hand();
     const size_t npix = (size_t)N * H * W;
     const size_t act = npix * 8 * 16 * 3;  // 64 channels at full resolution = the largest trunk tensor
-    uint8_t* A = h->x6A.ensure<uint8_t>(act, h->stream);
-    uint8_t* B = h->x6B.ensure<uint8_t>(act, h->stream);
+    uint8_t* A = h->w().x6A.ensure<uint8_t>(act, h->stream);
+    uint8_t* B = h->w().x6B.ensure<uint8_t>(act, h->stream);
     uint8_t* cur = nullptr;
     int cg = 1, hh = H, ww = W;
     for (size_t i = 0; i < vgg.size(); ++i) {
@@ -700,7 +722,7 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
             continue;
         }
         if (i == 0) {
-            uint8_t* X = h->x6in.ensure<uint8_t>(npix * 16 * 3, h->stream);
+            uint8_t* X = h->w().x6in.ensure<uint8_t>(npix * 16 * 3, h->stream);
             ProfEntry pe;
             h->prof_begin(pe, "to_x6", 0, (double)npix * (12 + 48));
             launch_to_x6(x, 3, 0, 3, N, H * W, X, 1, 0, (uint32_t)(npix * 16), h->stream);
@@ -747,10 +769,10 @@ static float* body_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
     const int hl = Hp / 8, wl = Wp / 8;
     const size_t px = (size_t)N * hl * wl;
     const int SG = 24, TG = 32, UG = 128;  // [L1 | L2 | trunk] = 5 + 3 + 16 groups; 256 / 1024 channels
-    uint8_t* S[2] = {h->x6S0.ensure<uint8_t>(px * SG * 48, h->stream), h->x6S1.ensure<uint8_t>(px * SG * 48, h->stream)};
-    uint8_t* T[2] = {h->x6T0.ensure<uint8_t>(px * TG * 48, h->stream), h->x6T1.ensure<uint8_t>(px * TG * 48, h->stream)};
-    uint8_t* U = h->x6U.ensure<uint8_t>(px * UG * 48, h->stream);
-    float* O = h->S0.ensure<float>(px * 185, h->stream);
+    uint8_t* S[2] = {h->w().x6S0.ensure<uint8_t>(px * SG * 48, h->stream), h->w().x6S1.ensure<uint8_t>(px * SG * 48, h->stream)};
+    uint8_t* T[2] = {h->w().x6T0.ensure<uint8_t>(px * TG * 48, h->stream), h->w().x6T1.ensure<uint8_t>(px * TG * 48, h->stream)};
+    uint8_t* U = h->w().x6U.ensure<uint8_t>(px * UG * 48, h->stream);
+    float* O = h->w().S0.ensure<float>(px * 185, h->stream);
     const int net = OPOSE_NET_BODY;
     auto s_ = [&](int i, int goff) { return x6act(S[i], SG, goff, px); };
     auto t_ = [&](int i, int goff) { return x6act(T[i], TG, goff, px); };
@@ -792,10 +814,10 @@ static float* hand_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
     const int hl = Hp / 8, wl = Wp / 8;
     const size_t px = (size_t)N * hl * wl;
     const int SG = 19, TG = 16, UG = 64;  // [L 22 + 2 | trunk 128] = 3 + 16 groups; 128 / 512 channels
-    uint8_t* S[2] = {h->x6S0.ensure<uint8_t>(px * SG * 48, h->stream), h->x6S1.ensure<uint8_t>(px * SG * 48, h->stream)};
-    uint8_t* T[2] = {h->x6T0.ensure<uint8_t>(px * TG * 48, h->stream), h->x6T1.ensure<uint8_t>(px * TG * 48, h->stream)};
-    uint8_t* U = h->x6U.ensure<uint8_t>(px * UG * 48, h->stream);
-    float* O = h->S0.ensure<float>(px * 150, h->stream);
+    uint8_t* S[2] = {h->w().x6S0.ensure<uint8_t>(px * SG * 48, h->stream), h->w().x6S1.ensure<uint8_t>(px * SG * 48, h->stream)};
+    uint8_t* T[2] = {h->w().x6T0.ensure<uint8_t>(px * TG * 48, h->stream), h->w().x6T1.ensure<uint8_t>(px * TG * 48, h->stream)};
+    uint8_t* U = h->w().x6U.ensure<uint8_t>(px * UG * 48, h->stream);
+    float* O = h->w().S0.ensure<float>(px * 150, h->stream);
     const int net = OPOSE_NET_HAND;
     auto s_ = [&](int i, int goff) { return x6act(S[i], SG, goff, px); };
     auto t_ = [&](int i) { return x6act(T[i], TG, 0, px); };
@@ -828,9 +850,9 @@ static float* body_net(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
     if (h->x6) return body_net_x6(h, x, N, Hp, Wp);
     const int hl = Hp / 8, wl = Wp / 8;
     const size_t px = (size_t)N * hl * wl;
-    float* S[2] = {h->S0.ensure<float>(px * 185, h->stream), h->S1.ensure<float>(px * 185, h->stream)};
-    float* T[2] = {h->T0.ensure<float>(px * 256, h->stream), h->T1.ensure<float>(px * 256, h->stream)};
-    float* U = h->U.ensure<float>(px * 1024, h->stream);
+    float* S[2] = {h->w().S0.ensure<float>(px * 185, h->stream), h->w().S1.ensure<float>(px * 185, h->stream)};
+    float* T[2] = {h->w().T0.ensure<float>(px * 256, h->stream), h->w().T1.ensure<float>(px * 256, h->stream)};
+    float* U = h->w().U.ensure<float>(px * 1024, h->stream);
     const int net = OPOSE_NET_BODY;
     run_trunk(h, net, x, N, Hp, Wp, Act{S[0], 185, 57}, Act{S[1], 185, 57});
     // stage 1 (src/model.py:52-62): input = trunk slice of S0
@@ -872,9 +894,9 @@ static float* hand_net(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
     if (h->x6) return hand_net_x6(h, x, N, Hp, Wp);
     const int hl = Hp / 8, wl = Wp / 8;
     const size_t px = (size_t)N * hl * wl;
-    float* S[2] = {h->S0.ensure<float>(px * 150, h->stream), h->S1.ensure<float>(px * 150, h->stream)};
-    float* T[2] = {h->T0.ensure<float>(px * 128, h->stream), h->T1.ensure<float>(px * 128, h->stream)};
-    float* U = h->U.ensure<float>(px * 512, h->stream);
+    float* S[2] = {h->w().S0.ensure<float>(px * 150, h->stream), h->w().S1.ensure<float>(px * 150, h->stream)};
+    float* T[2] = {h->w().T0.ensure<float>(px * 128, h->stream), h->w().T1.ensure<float>(px * 128, h->stream)};
+    float* U = h->w().U.ensure<float>(px * 512, h->stream);
     const int net = OPOSE_NET_HAND;
     run_trunk(h, net, x, N, Hp, Wp, Act{S[0], 150, 22}, Act{S[1], 150, 22});
     run_conv(h, find_conv(h, net, "conv6_1_CPM"), nullptr, N, hl, wl, Act{S[0], 150, 22}, Act{U, 512, 0}, Act{},
@@ -1335,7 +1357,7 @@ static int net_forward(opose_t* h, int net, const float* x, int N, int Hp, int W
         const size_t in_n = (size_t)N * 3 * Hp * Wp;
         const float* xd = x;
         if (!(flags & OPOSE_IN_DEVICE)) {
-            float* buf = h->x.ensure<float>(in_n, h->stream);
+            float* buf = h->w().x.ensure<float>(in_n, h->stream);
             OPOSE_HIP_CHECK(hipMemcpyAsync(buf, x, in_n * 4, hipMemcpyHostToDevice, h->stream));
             xd = buf;
         }
@@ -1459,7 +1481,7 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
         auto net_part = [&] {
             for (int s = 0; s < p.n_scales; ++s) {
                 const ScaleGeom& g = gs[s];
-                float* x = h->x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
+                float* x = h->w().x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
                 ProfEntry pe;
                 h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
                 launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp,
@@ -1551,7 +1573,7 @@ int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, i
             fd = buf;
         }
         const ScaleGeom g = geom(p.scales[s], p, H, W);
-        float* x = h->x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
+        float* x = h->w().x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
         launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp, g.Wp,
                           (float)p.pad_value / 256.f - 0.5f, x, h->stream);
         const float* S = body_net(h, x, N, g.Hp, g.Wp);
@@ -1633,7 +1655,7 @@ int opose_batch_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, 
                                                   : h->records.ensure<uint8_t>(L.bytes * N, h->stream);
         const std::string key = call_key("batch_body", N, H, W, row_stride, frame_stride, p, fd, rec, h->ppp, h->maxp);
         run_graphed(h, key, [&] {
-            float* x = h->x.ensure<float>((size_t)N * 3 * Hp * Wp, h->stream);
+            float* x = h->w().x.ensure<float>((size_t)N * 3 * Hp * Wp, h->stream);
             ProfEntry pe;
             h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * Hp * Wp));
             const float sc = (float)(1.0 / scale);  // torch: float(1 / scale_factor)
@@ -1704,6 +1726,37 @@ static void hand_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
 }
 
 // copy the hand results to the host (unless they were written to device buffers)
+// fn(s) for every scale s, scale s on stream s (0: the handle's stream, others its scale
+// streams), each with workspace slot s; the handle's stream continues after all of them
+static void run_scales_concurrently(opose_ctx* h, int ns, const std::function<void(int)>& fn) {
+    const hipStream_t main = h->stream;
+    if (!h->ev_fork) OPOSE_HIP_CHECK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    OPOSE_HIP_CHECK(hipEventRecord(h->ev_fork, main));
+    for (int s = 1; s < ns; ++s) {
+        if (!h->sstream[s]) {
+            OPOSE_HIP_CHECK(hipStreamCreateWithFlags(&h->sstream[s], hipStreamNonBlocking));
+            OPOSE_HIP_CHECK(hipEventCreateWithFlags(&h->ev_join[s], hipEventDisableTiming));
+        }
+        OPOSE_HIP_CHECK(hipStreamWaitEvent(h->sstream[s], h->ev_fork, 0));
+    }
+    // largest scale first: it is the critical path
+    try {
+        for (int s = ns - 1; s >= 0; --s) {
+            h->stream = s ? h->sstream[s] : main;
+            h->slot = s;
+            fn(s);
+            if (s) OPOSE_HIP_CHECK(hipEventRecord(h->ev_join[s], h->sstream[s]));
+        }
+    } catch (...) {
+        h->stream = main;
+        h->slot = 0;
+        throw;
+    }
+    h->stream = main;
+    h->slot = 0;
+    for (int s = 1; s < ns; ++s) OPOSE_HIP_CHECK(hipStreamWaitEvent(main, h->ev_join[s], 0));
+}
+
 static void hand_finish(opose_ctx* h, int N, double* peaks_out, int32_t* found_out, int flags) {
     const int NP = N * 21;
     if (!(flags & OPOSE_OUT_DEVICE)) {
@@ -1737,20 +1790,28 @@ int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
         std::snprintf(fk, sizeof fk, "%p", od ? (const void*)found : nullptr);
         const std::string key =
             call_key("hand", N, H, W, row_stride, frame_stride, p, fd, od ? (const void*)peaks : nullptr, 0, 0) + fk;
-        run_graphed(h, key, [&] {
-            for (int s = 0; s < p.n_scales; ++s) {
-                const ScaleGeom& g = gs[s];
-                float* x = h->x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
-                ProfEntry pe;
-                h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
-                launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp,
-                                  g.Wp, (float)p.pad_value / 256.f - 0.5f, x, h->stream);
-                h->prof_end(pe);
-                float* Sb = hand_net(h, x, N, g.Hp, g.Wp);
-                upsample_to_mid(h, s, Sb, 150, N, g, 21);
-            }
+        auto scale_net = [&](int s) {
+            const ScaleGeom& g = gs[s];
+            float* x = h->w().x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
+            ProfEntry pe;
+            h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
+            launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp,
+                              g.Wp, (float)p.pad_value / 256.f - 0.5f, x, h->stream);
+            h->prof_end(pe);
+            float* Sb = hand_net(h, x, N, g.Hp, g.Wp);
+            upsample_to_mid(h, s, Sb, 150, N, g, 21);
+        };
+        if (h->scale_streams && p.n_scales > 1) {
+            // the scales' networks are independent until the heat average: each on its own stream
+            // with its own workspace (a single crop's layers fill a fraction of the chip each)
+            run_scales_concurrently(h, p.n_scales, scale_net);
             hand_post_common(h, N, H, W, gs, p, peaks, found, flags & OPOSE_OUT_DEVICE);
-        });
+        } else {
+            run_graphed(h, key, [&] {
+                for (int s = 0; s < p.n_scales; ++s) scale_net(s);
+                hand_post_common(h, N, H, W, gs, p, peaks, found, flags & OPOSE_OUT_DEVICE);
+            });
+        }
         hand_finish(h, N, peaks, found, flags & OPOSE_OUT_DEVICE);
     });
     return OPOSE_OK;
@@ -1817,7 +1878,7 @@ int opose_batch_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, 
             fd = buf;
         }
         // ToTensor - 0.5 at scale 1 (torch bicubic at scale 1 is the identity)
-        float* x = h->x.ensure<float>((size_t)N * 3 * H * W, h->stream);
+        float* x = h->w().x.ensure<float>((size_t)N * 3 * H * W, h->stream);
         ProfEntry pe;
         h->prof_begin(pe, "preprocess", 0, (double)N * 15.0 * H * W);
         launch_preprocess_torch(fd, frame_stride, row_stride, N, H, W, H, W, 1.f, 1.f, H, W, x, h->stream);
@@ -1859,7 +1920,7 @@ int opose_hand_infer_crops(opose_t* h, const uint8_t* const* crops, const int* s
         }
         for (int s = 0; s < ns; ++s) {
             const ScaleGeom& g0 = gs[0][s];
-            float* x = h->x.ensure<float>((size_t)n * 3 * g0.Hp * g0.Wp, h->stream);
+            float* x = h->w().x.ensure<float>((size_t)n * 3 * g0.Hp * g0.Wp, h->stream);
             ProfEntry pe;
             h->prof_begin(pe, "preprocess", 0, 0);
             for (int i = 0; i < n; ++i) {
@@ -1957,7 +2018,7 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
         if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
         a.ngroups = 1;
         a.sk_grid = t.grid;
-        a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
         a.sk_cnt = h->sk_counters((a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * a.ngroups);
         if (!(h->conv_window && launch_conv_window(a, t.mt, t.pt, h->stream))) launch_conv(a, c->ktab, t.mt, t.pt, h->stream);
         OPOSE_HIP_CHECK(hipMemcpyAsync(out, yd, ny * 4, hipMemcpyDeviceToHost, h->stream));
@@ -2003,7 +2064,7 @@ int opose_debug_conv_x6(opose_t* h, const float* x, const float* w, const float*
         if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
         a.ngroups = 1;
         a.sk_grid = t.grid;
-        a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
         launch_conv_x6(a, t.mt, t.pt, h->stream);
         if (out_x6) launch_from_x6(y6, og, 0, ops, Cout, N, HW, yd, Cout, 0, h->stream);
         OPOSE_HIP_CHECK(hipMemcpyAsync(out, yd, ny * 4, hipMemcpyDeviceToHost, h->stream));
@@ -2050,7 +2111,7 @@ int opose_debug_conv_x6_time(opose_t* h, int N, int Cin, int H, int W, int Cout,
         if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
         a.ngroups = ngroups;
         a.sk_grid = t.grid;
-        a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
         if (const char* ab = getenv("OPOSE_X6_ABLATE")) a.ablate = atoi(ab);
         launch_conv_x6(a, t.mt, t.pt, h->stream);  // warm-up
         hipEvent_t e0, e1;
@@ -2104,7 +2165,7 @@ int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, in
         if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
         a.ngroups = ngroups;
         a.sk_grid = t.grid;
-        a.partial = h->partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
         a.sk_cnt = h->sk_counters((a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * a.ngroups);
         auto go = [&]() {
             if (ablate) {
