@@ -1414,6 +1414,37 @@ static opose_params fill_params(const opose_params* p, int net) {
 }
 
 namespace opose {
+// fn(s) for every scale s, scale s on stream s (0: the handle's stream, others its scale
+// streams), each with workspace slot s; the handle's stream continues after all of them
+static void run_scales_concurrently(opose_ctx* h, int ns, const std::function<void(int)>& fn) {
+    const hipStream_t main = h->stream;
+    if (!h->ev_fork) OPOSE_HIP_CHECK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    OPOSE_HIP_CHECK(hipEventRecord(h->ev_fork, main));
+    for (int s = 1; s < ns; ++s) {
+        if (!h->sstream[s]) {
+            OPOSE_HIP_CHECK(hipStreamCreateWithFlags(&h->sstream[s], hipStreamNonBlocking));
+            OPOSE_HIP_CHECK(hipEventCreateWithFlags(&h->ev_join[s], hipEventDisableTiming));
+        }
+        OPOSE_HIP_CHECK(hipStreamWaitEvent(h->sstream[s], h->ev_fork, 0));
+    }
+    // largest scale first: it is the critical path
+    try {
+        for (int s = ns - 1; s >= 0; --s) {
+            h->stream = s ? h->sstream[s] : main;
+            h->slot = s;
+            fn(s);
+            if (s) OPOSE_HIP_CHECK(hipEventRecord(h->ev_join[s], h->sstream[s]));
+        }
+    } catch (...) {
+        h->stream = main;
+        h->slot = 0;
+        throw;
+    }
+    h->stream = main;
+    h->slot = 0;
+    for (int s = 1; s < ns; ++s) OPOSE_HIP_CHECK(hipStreamWaitEvent(main, h->ev_join[s], 0));
+}
+
 static void pipelined_body(opose_ctx* h, int N, int H, int W, const std::vector<ScaleGeom>& gs,
                            const opose_params& p, uint8_t* rec, const std::function<void()>& net_part) {
     if (!h->nstream) {
@@ -1478,21 +1509,27 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
         for (int s = 0; s < p.n_scales; ++s) gs.push_back(geom(p.scales[s], p, H, W));
         uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)
                                                   : h->records.ensure<uint8_t>(L.bytes * N, h->stream);
+        auto scale_net = [&](int s) {
+            const ScaleGeom& g = gs[s];
+            float* x = h->w().x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
+            ProfEntry pe;
+            h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
+            launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp,
+                              g.Wp, (float)p.pad_value / 256.f - 0.5f, x, h->stream);
+            h->prof_end(pe);
+            float* S = body_net(h, x, N, g.Hp, g.Wp);
+            upsample_to_mid(h, s, S, 185, N, g, 56);
+        };
         auto net_part = [&] {
-            for (int s = 0; s < p.n_scales; ++s) {
-                const ScaleGeom& g = gs[s];
-                float* x = h->w().x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
-                ProfEntry pe;
-                h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
-                launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp,
-                                  g.Wp, (float)p.pad_value / 256.f - 0.5f, x, h->stream);
-                h->prof_end(pe);
-                float* S = body_net(h, x, N, g.Hp, g.Wp);
-                upsample_to_mid(h, s, S, 185, N, g, 56);
-            }
+            for (int s = 0; s < p.n_scales; ++s) scale_net(s);
         };
         if (h->pipeline && (flags & OPOSE_PIPELINE) && (flags & OPOSE_IN_DEVICE) && (flags & OPOSE_OUT_DEVICE)) {
             pipelined_body(h, N, H, W, gs, p, rec, net_part);
+        } else if (h->scale_streams && p.n_scales > 1) {  // multi-scale pyramid (C5): scales concurrently
+            enter_main(h);
+            h->mid_set = 0;
+            run_scales_concurrently(h, p.n_scales, scale_net);
+            body_post_common(h, N, H, W, gs, p, rec);
         } else {
             enter_main(h);
             h->mid_set = 0;
@@ -1726,37 +1763,6 @@ static void hand_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
 }
 
 // copy the hand results to the host (unless they were written to device buffers)
-// fn(s) for every scale s, scale s on stream s (0: the handle's stream, others its scale
-// streams), each with workspace slot s; the handle's stream continues after all of them
-static void run_scales_concurrently(opose_ctx* h, int ns, const std::function<void(int)>& fn) {
-    const hipStream_t main = h->stream;
-    if (!h->ev_fork) OPOSE_HIP_CHECK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-    OPOSE_HIP_CHECK(hipEventRecord(h->ev_fork, main));
-    for (int s = 1; s < ns; ++s) {
-        if (!h->sstream[s]) {
-            OPOSE_HIP_CHECK(hipStreamCreateWithFlags(&h->sstream[s], hipStreamNonBlocking));
-            OPOSE_HIP_CHECK(hipEventCreateWithFlags(&h->ev_join[s], hipEventDisableTiming));
-        }
-        OPOSE_HIP_CHECK(hipStreamWaitEvent(h->sstream[s], h->ev_fork, 0));
-    }
-    // largest scale first: it is the critical path
-    try {
-        for (int s = ns - 1; s >= 0; --s) {
-            h->stream = s ? h->sstream[s] : main;
-            h->slot = s;
-            fn(s);
-            if (s) OPOSE_HIP_CHECK(hipEventRecord(h->ev_join[s], h->sstream[s]));
-        }
-    } catch (...) {
-        h->stream = main;
-        h->slot = 0;
-        throw;
-    }
-    h->stream = main;
-    h->slot = 0;
-    for (int s = 1; s < ns; ++s) OPOSE_HIP_CHECK(hipStreamWaitEvent(main, h->ev_join[s], 0));
-}
-
 static void hand_finish(opose_ctx* h, int N, double* peaks_out, int32_t* found_out, int flags) {
     const int NP = N * 21;
     if (!(flags & OPOSE_OUT_DEVICE)) {

@@ -28,12 +28,16 @@ from src.weights import BENCH_OUT_SCALE, c5_out_scale, seeded_state_dict  # noqa
 
 
 def timed(fn, iters, warm=2):
+    """Median wall time of fn() with the device drained after each call (device-tensor entry
+    points return asynchronously, ordered on torch's current stream)."""
     for _ in range(warm):
         fn()
+    torch.cuda.synchronize()
     t = []
     for _ in range(iters):
         t0 = time.perf_counter()
         fn()
+        torch.cuda.synchronize()
         t.append(time.perf_counter() - t0)
     return float(np.median(t)) * 1e3
 
