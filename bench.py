@@ -137,6 +137,12 @@ def stage_roofline(prof):
             a = px * GAUSS_OPS_PER_PIXEL / (v["ms"] * 1e-3)
             out[k] = {"bound": "valu_f64", "achieved": round(a / 1e12, 2), "peak": PEAK_F64_OPS / 1e12,
                       "unit": "T float64 ops/s", "frac": round(a / PEAK_F64_OPS, 4)}
+        elif k == "gauss_nms_resize" and v.get("flops", 0) > 0:
+            # the same filter with the heat-map resize fused in (csrc/post.hip gauss_nms_resize):
+            # flops recorded per launch = GAUSS_OPS_PER_PIXEL x full-resolution map pixels
+            a = v["flops"] / (v["ms"] * 1e-3)
+            out[k] = {"bound": "valu_f64", "achieved": round(a / 1e12, 2), "peak": PEAK_F64_OPS / 1e12,
+                      "unit": "T float64 ops/s", "frac": round(a / PEAK_F64_OPS, 4)}
         elif k in LATENCY_STAGES or v.get("bytes", 0) <= 0:
             out[k] = {"bound": "latency", "achieved": None, "peak": None, "unit": None, "frac": None}
         else:

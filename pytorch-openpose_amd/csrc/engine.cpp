@@ -211,6 +211,14 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_CONV12_FUSED");
         return e && e[0] == '1';
     }();
+    // single-scale Body: the heat-map resize fused into the NMS tiles (gauss_nms_resize, post.hip),
+    // opt-in (OPOSE_FUSE_HEAT=1): bit-identical, but 1.10 ms per bench step against 0.47 + 0.43 ms
+    // for heat_full_f32 + gauss_nms_wide (the tiles' halos redo 2.3x the resize arithmetic, and
+    // gfx950 issues float32 VALU at the float64 rate)
+    bool fuse_heat = [] {
+        const char* e = getenv("OPOSE_FUSE_HEAT");
+        return e && e[0] == '1';
+    }();
     DevBuf frames, mids[2][kMaxScales], avg, cnt, list, peak_pos, part_cnt, score, conn, conn_cnt, records, maps_in,
         hlab, hsums, hpeaks, hfound, list_score, hsel;
     // network workspace, one set per concurrently running scale (slot s runs on scale_stream(s);
@@ -978,7 +986,16 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * N * 18, h->stream));
     ProfEntry pe;
     // single scale: the float64 average equals the float32 resize output exactly -> f32 map
+    // (fuse_heat: the resize runs inside the NMS tiles, no full-resolution map at all)
     const bool f32 = ns == 1;
+    if (f32 && h->fuse_heat && gauss_nms_resize_fits(gs[0].Hs, gs[0].Ws, H, W, gs[0].up_sy)) {
+        // flops: the filter's float64 operations (2 x 37 per map pixel, bench.py GAUSS_OPS_PER_PIXEL);
+        // bytes: the x8 heat channels read
+        h->prof_begin(pe, "gauss_nms_resize", (double)N * 18 * 74.0 * H * W, (double)N * 18 * 4.0 * gs[0].Hs * gs[0].Ws);
+        launch_gauss_nms_resize(S.mid[0], 56, 38, 18, N, gs[0].Hs, gs[0].Ws, H, W, gs[0].up_sy, gs[0].up_sx, p.thre1,
+                                cap, cnt, list, lscore, h->stream);
+        h->prof_end(pe);
+    } else {
     double* avg = h->avg.ensure<double>((size_t)N * 18 * H * W, h->stream);
     for (int s = 0; s < ns; ++s) {
         h->prof_begin(pe, "heat_full", 0,
@@ -994,6 +1011,7 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     h->prof_begin(pe, "gauss_nms", 0, (double)N * 18 * H * W * (f32 ? 4 : 8));
     launch_gauss_nms(avg, f32, N * 18, H, W, p.thre1, cap, cnt, list, lscore, h->stream);
     h->prof_end(pe);
+    }
     h->prof_begin(pe, "peaks_finalize", 0, 0);
     launch_peaks_finalize(cnt, list, lscore, N, H, W, L, rec_dev, pos, pcnt, h->stream);
     h->prof_end(pe);

@@ -100,6 +100,7 @@ __global__ __launch_bounds__(256) void heat_full_accum(const float* __restrict__
 // 2: float64 heat average (+)= (double)(v/ns).
 constexpr int RS_RT = 16;      // output rows per workgroup
 constexpr int RS_MAXR = 44;    // staged source rows (RT * scale + 5 <= 44  <=>  scale <= 2.4)
+constexpr int RS_CHUNK = 8;    // staged rows loaded per round
 
 // MAXR: LDS rows actually staged (8 for x8, 16 for x2): small tiles keep many workgroups
 // resident, which this HBM-bound kernel needs
@@ -124,13 +125,25 @@ __global__ __launch_bounds__(256) void cubic_resize_rows(const float* __restrict
     if (tid < y1 - y0) s_ty[tid] = cubic_tap_any(y0 + tid, sy, hi, torch);
     if (live) {
         const CubicTap tx = cubic_tap_any(x, sx, wi, torch);
-        for (int r = r_lo; r <= r_hi; ++r) {
-            const float* row = plane + (size_t)r * wi;
-            float v = row[tx.i[0]] * tx.c[0];
-            v = v + row[tx.i[1]] * tx.c[1];
-            v = v + row[tx.i[2]] * tx.c[2];
-            v = v + row[tx.i[3]] * tx.c[3];
-            hs[r - r_lo][tid] = v;
+        // RS_CHUNK rows per round with every load issued before the first use (rows past r_hi
+        // re-read r_hi and are not stored): a row-at-a-time loop waited out one memory round
+        // trip per staged row
+        for (int k0 = 0; k0 < MAXR && r_lo + k0 <= r_hi; k0 += RS_CHUNK) {
+            float p[RS_CHUNK][4];
+#pragma unroll
+            for (int k = 0; k < RS_CHUNK; ++k) {
+                const float* row = plane + (size_t)min(r_lo + k0 + k, r_hi) * wi;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) p[k][j] = row[tx.i[j]];
+            }
+#pragma unroll
+            for (int k = 0; k < RS_CHUNK; ++k) {
+                float v = p[k][0] * tx.c[0];
+                v = v + p[k][1] * tx.c[1];
+                v = v + p[k][2] * tx.c[2];
+                v = v + p[k][3] * tx.c[3];
+                if (k0 + k < MAXR && r_lo + k0 + k <= r_hi) hs[k0 + k][tid] = v;
+            }
         }
     }
     __syncthreads();

@@ -67,6 +67,12 @@ void launch_resize_torch_f32(const float* mid, int Cm, int coff, int P, int N, i
 // post.hip
 void launch_gauss_nms(const void* avg, bool f32, int NP, int H, int W, double thre, int cap, int* cnt, int* list,
                       double* list_score, hipStream_t st);
+// single scale: heat_full's resize of mid channels [coff, coff+P) fused into the wide NMS
+// (requires gauss_nms_resize_fits: a true resize with source step sy <= 0.618)
+bool gauss_nms_resize_fits(int Hs, int Ws, int H, int W, double sy);
+void launch_gauss_nms_resize(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
+                             double sx, double thre, int cap, int* cnt, int* list, double* list_score,
+                             hipStream_t st);
 // Batch_body fast mode: 5x5 Gaussian (reflect pad, srcmx/utilmx.py:246-263) + findpeaks_torch
 // (srcmx/utilmx.py:230-243) on heat [NP][H][W] float; scores = blurred values
 void launch_blur5_nms(const float* heat, int NP, int H, int W, double thre, int cap, int* cnt, int* list,

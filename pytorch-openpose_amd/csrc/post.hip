@@ -1,4 +1,5 @@
 #include <cstdlib>
+#include <stdexcept>
 // post.hip — the post-network Body path as wavefront-parallel kernels.
 //
 // Reference (hitmaxiang/pytorch-openpose src/body.py), all float64 like the reference:
@@ -177,32 +178,16 @@ __device__ __forceinline__ void gauss_wide_load(const T* __restrict__ m, int H, 
     }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void gauss_nms_wide(const T* __restrict__ avg, int H, int W, double thre, int cap,
-                                                      int* __restrict__ cnt, int* __restrict__ list,
-                                                      double* __restrict__ list_score) {
-    __shared__ double sv[WVR][WVW + 1];
-    int x0, y0, np;
-    {
-        const int ntx = (W + WTW - 1) / WTW, nty = (H + WTH - 1) / WTH;
-        const int total = gridDim.x, b = blockIdx.x;
-        const int q = total >> 3, rr = total & 7, xcd = b & 7;
-        const int id = xcd * q + min(xcd, rr) + (b >> 3);  // XCD-contiguous tile ranges (guide T1)
-        const int tx = id % ntx, rest = id / ntx;
-        x0 = tx * WTW;
-        y0 = (rest % nty) * WTH;
-        np = rest / nty;
-    }
-    const T* m = avg + (size_t)np * H * W;
+// smoothing + NMS of one wide tile from the vertical pass's register window (every thread of
+// the workgroup calls it; sv may alias a staging buffer the window was built from: the first
+// barrier below comes after every window is complete).  score_at(y, x) = map_ori[y, x].
+template <typename ScoreAt>
+__device__ __forceinline__ void gauss_wide_tail(double (&win)[WVH + 24], double (*sv)[WVW + 1], int H, int W, int x0,
+                                                int y0, int np, double thre, int cap, int* __restrict__ cnt,
+                                                int* __restrict__ list, double* __restrict__ list_score,
+                                                ScoreAt score_at) {
     const int tid = threadIdx.x;
     const int c = tid & (WVW - 1), h = tid >> 7;
-    double win[WVH + 24];
-    if (x0 >= 13 && x0 + WTW + 13 <= W && y0 >= 13 && y0 + WTH + 13 <= H)
-        gauss_wide_load<T, 0>(m, H, W, x0, y0, c, h, win);
-    else if (x0 - 13 >= -W && x0 + WTW + 13 <= 2 * W && y0 - 13 >= -H && y0 + WTH + 13 <= 2 * H)
-        gauss_wide_load<T, 1>(m, H, W, x0, y0, c, h, win);
-    else
-        gauss_wide_load<T, 2>(m, H, W, x0, y0, c, h, win);
     bool hot = false;
     const double skip_below = gauss_skip_below(thre);
 #pragma unroll
@@ -244,10 +229,130 @@ __global__ __launch_bounds__(256) void gauss_nms_wide(const T* __restrict__ avg,
             const int slot = atomicAdd(cnt + np, 1);
             if (slot < cap) {
                 list[(size_t)np * cap + slot] = y * W + x;
-                list_score[(size_t)np * cap + slot] = (double)m[(size_t)y * W + x];  // map_ori[y, x]
+                list_score[(size_t)np * cap + slot] = score_at(y, x);
             }
         }
     }
+}
+
+// wide tile id -> (x0, y0, map) in XCD-contiguous ranges (guide T1)
+__device__ __forceinline__ void gauss_wide_coords(int H, int W, int& x0, int& y0, int& np) {
+    const int ntx = (W + WTW - 1) / WTW, nty = (H + WTH - 1) / WTH;
+    const int total = gridDim.x, b = blockIdx.x;
+    const int q = total >> 3, rr = total & 7, xcd = b & 7;
+    const int id = xcd * q + min(xcd, rr) + (b >> 3);
+    const int tx = id % ntx, rest = id / ntx;
+    x0 = tx * WTW;
+    y0 = (rest % nty) * WTH;
+    np = rest / nty;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gauss_nms_wide(const T* __restrict__ avg, int H, int W, double thre, int cap,
+                                                      int* __restrict__ cnt, int* __restrict__ list,
+                                                      double* __restrict__ list_score) {
+    __shared__ double sv[WVR][WVW + 1];
+    int x0, y0, np;
+    gauss_wide_coords(H, W, x0, y0, np);
+    const T* m = avg + (size_t)np * H * W;
+    const int tid = threadIdx.x;
+    const int c = tid & (WVW - 1), h = tid >> 7;
+    double win[WVH + 24];
+    if (x0 >= 13 && x0 + WTW + 13 <= W && y0 >= 13 && y0 + WTH + 13 <= H)
+        gauss_wide_load<T, 0>(m, H, W, x0, y0, c, h, win);
+    else if (x0 - 13 >= -W && x0 + WTW + 13 <= 2 * W && y0 - 13 >= -H && y0 + WTH + 13 <= 2 * H)
+        gauss_wide_load<T, 1>(m, H, W, x0, y0, c, h, win);
+    else
+        gauss_wide_load<T, 2>(m, H, W, x0, y0, c, h, win);
+    gauss_wide_tail(win, sv, H, W, x0, y0, np, thre, cap, cnt, list, list_score,
+                    [&](int y, int x) { return (double)m[(size_t)y * W + x]; });
+}
+
+// Single-scale Body path with heat_full's cubic resize (src/body.py:57) fused in: the NMS window
+// is resized from the x8 map (mid) inside the tile, so the full-resolution float32 map is neither
+// written nor re-read (8 bytes per pixel and part).  The footprint's source rows are resized
+// horizontally once into LDS (aliasing the smoothing plane), then each vertical-pass thread
+// combines its 40 window rows from them -- cubic_resize_rows<1>'s arithmetic in its order, so the
+// window holds exactly the values launch_heat_full_f32 would have stored (0.f + v).  The score of
+// a peak (map_ori[y, x]) is resampled from mid with cubic_sample_f32 (bit-identical, rare).
+constexpr int GR_FOOT = WVR + 24;  // 56 footprint rows
+constexpr int GR_MAXR = 40;        // staged source rows: 55 * sy + 6 <= 40
+static_assert(GR_MAXR * WVW * 4 <= WVR * (WVW + 1) * 8, "staged rows fit in the smoothing plane");
+
+__global__ __launch_bounds__(256) void gauss_nms_resize(const float* __restrict__ mid, int Cm, int coff, int P, int Hs,
+                                                        int Ws, int H, int W, double sy, double sx, double thre,
+                                                        int cap, int* __restrict__ cnt, int* __restrict__ list,
+                                                        double* __restrict__ list_score) {
+    __shared__ double sv[WVR][WVW + 1];
+    __shared__ CubicTap s_ty[GR_FOOT];
+    __shared__ int s_lo, s_hi;
+    float (*hs)[WVW] = reinterpret_cast<float (*)[WVW]>(&sv[0][0]);
+    int x0, y0, np;
+    gauss_wide_coords(H, W, x0, y0, np);
+    const int n = np / P, p = np - n * P;
+    const float* plane = mid + ((size_t)n * Cm + coff + p) * Hs * Ws;
+    const int tid = threadIdx.x;
+    const int c = tid & (WVW - 1), h = tid >> 7;
+    if (tid == 0) {
+        s_lo = 0x7fffffff;
+        s_hi = -1;
+    }
+    __syncthreads();
+    if (tid < GR_FOOT) {  // vertical taps of the footprint rows (reflected like scipy)
+        const CubicTap ty = cubic_tap(reflect_idx(y0 - 13 + tid, H), sy, Hs);
+        s_ty[tid] = ty;
+        atomicMin(&s_lo, ty.i[0]);
+        atomicMax(&s_hi, ty.i[3]);
+    }
+    __syncthreads();
+    const int lo = s_lo, hi = s_hi;
+    {
+        const CubicTap tx = cubic_tap(reflect_idx(x0 - 13 + c, W), sx, Ws);
+        for (int r0 = lo + h; r0 <= hi; r0 += 16) {  // 8 rows per round, loads issued first
+            float q[8][4];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float* row = plane + (size_t)min(r0 + 2 * k, hi) * Ws;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) q[k][j] = row[tx.i[j]];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                float v = q[k][0] * tx.c[0];
+                v = v + q[k][1] * tx.c[1];
+                v = v + q[k][2] * tx.c[2];
+                v = v + q[k][3] * tx.c[3];
+                if (r0 + 2 * k <= hi) hs[r0 + 2 * k - lo][c] = v;
+            }
+        }
+    }
+    __syncthreads();
+    double win[WVH + 24];
+#pragma unroll
+    for (int i = 0; i < WVH + 24; ++i) {
+        const CubicTap ty = s_ty[h * WVH + i];
+        float o = hs[ty.i[0] - lo][c] * ty.c[0];
+        o = o + hs[ty.i[1] - lo][c] * ty.c[1];
+        o = o + hs[ty.i[2] - lo][c] * ty.c[2];
+        o = o + hs[ty.i[3] - lo][c] * ty.c[3];
+        win[i] = (double)(0.f + o);
+    }
+    gauss_wide_tail(win, sv, H, W, x0, y0, np, thre, cap, cnt, list, list_score, [&](int y, int x) {
+        return (double)(0.f + cubic_sample_f32(plane, Ws, cubic_tap(y, sy, Hs), cubic_tap(x, sx, Ws)));
+    });
+}
+
+bool gauss_nms_resize_fits(int Hs, int Ws, int H, int W, double sy) {
+    return !(Hs == H && Ws == W) && 55.0 * sy + 6.0 <= (double)GR_MAXR;
+}
+
+void launch_gauss_nms_resize(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
+                             double sx, double thre, int cap, int* cnt, int* list, double* list_score,
+                             hipStream_t st) {
+    if (!gauss_nms_resize_fits(Hs, Ws, H, W, sy)) throw std::invalid_argument("gauss_nms_resize: scale out of range");
+    const int tiles = ((W + WTW - 1) / WTW) * ((H + WTH - 1) / WTH) * N * P;
+    hipLaunchKernelGGL(gauss_nms_resize, dim3(tiles), dim3(256), 0, st, mid, Cm, coff, P, Hs, Ws, H, W, sy, sx, thre,
+                       cap, cnt, list, list_score);
 }
 
 // Hand: binary = gaussian_filter(map) > thre (src/hand.py:62-63) as union-find seeds:
