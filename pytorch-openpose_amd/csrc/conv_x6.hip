@@ -1449,6 +1449,216 @@ void launch_conv12_pool_x6(const float* x, int N, int H, int W, const float* w11
                        out, ops, abl);
 }
 
+// ---------------------------------------------------------------- windowed conv1_2 (+ pool)
+// conv1_2 (64 -> 64 channels, 3x3, pad 1) + MaxPool2d(2, 2) from conv1_1's X6 tensor, with the
+// im2col operand replaced by a window (src/model.py:35-37 / :145-147).  conv_x6 streams each
+// input unit through L2 -> LDS once per tap (9x) and, at M = 64, once per 64 output channels:
+// 442 KB of im2col + 221 KB of weights per 64 x 128 tile, 10 GB per bench step.  Here a
+// workgroup owns an 8 x 16 tile of conv1_2 outputs (4 x 8 pooled pixels) of one frame and, per
+// channel block (4 groups = 32 channels), DMAs the 10 x 18 input window once (69 KB per tile for
+// both blocks) and reads the nine taps' B fragments from it at the tap's offset:
+//  * window [piece][group][row (pitch 24 units)][col]: the pitch (== 8 mod 16 units) and the
+//    group pitch (== 0 mod 16) put every ds_read_b128 lane group on 16 distinct bank quads (as
+//    conv12_pool_x6); the pad columns 18..23 and the frame border load zeros through the buffer
+//    range check (conv1_2's zero padding);
+//  * 18 k-chunks (2 channel blocks x 9 taps) in the weight layout of conv_x6 (one chunk = 12
+//    (piece, group) rows of 64 units), two weight stages by LDS-DMA, one barrier per chunk;
+//    4 waves, each 64 channels x 32 GEMM columns (one pooled row of 8 pixels x their 4
+//    quadrants): every A fragment read serves two column blocks (8 waves of 16 columns read
+//    245 KB of LDS per chunk and CU, more than the MFMAs take at 128 B/clk); the six piece
+//    products in conv_x6's MODE 2 order: bit-identical to the conv_x6 pooled launch;
+//  * the fragments of chunk c + 1 are read during chunk c's MFMAs (two register sets); the second
+//    block's window is DMA'd over the first block's buffer behind chunk 8's MFMAs;
+//  * 70 KB of LDS: two workgroups per CU cover each other's DMA waits, barriers and epilogues.
+namespace {
+constexpr int V_TH = 8, V_TW = 16;                 // conv1_2 outputs per tile
+constexpr int V_WR = V_TH + 2, V_WC = V_TW + 2;    // window 10 x 18
+constexpr int V_RP = 24;                           // window row pitch (units)
+constexpr int V_GP = V_WR * V_RP;                  // 240 units per channel group
+constexpr int V_PP = 4 * V_GP;                     // 960 units per piece (one channel block)
+constexpr int V_WIN = 3 * V_PP;                    // 2880 units
+constexpr int V_DMA = V_WIN / 64;                  // 45 window DMA instructions
+constexpr int V_NW = 4;                            // waves: 64 channels x 32 GEMM columns each
+static_assert(V_RP % 16 == 8 && V_GP % 16 == 0 && V_RP >= V_WC && V_PP % 64 == 0, "conv1_2 window pitches");
+struct WinSmem {
+    uint4 win[V_WIN];
+    uint4 a[2][12 * 64];
+    float b[64];
+};
+}  // namespace
+
+__global__ __launch_bounds__(256, 2) void conv3_pool_win_x6_kernel(const uint8_t* __restrict__ in, uint32_t ips,
+                                                                   int N, int H, int W,
+                                                                   const uint8_t* __restrict__ wt,
+                                                                   const float* __restrict__ bias,
+                                                                   uint8_t* __restrict__ out, uint32_t ops) {
+    __shared__ WinSmem sm;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ntx = (W + V_TW - 1) / V_TW, nty = (H + V_TH - 1) / V_TH;
+    int n, y0, x0;
+    {
+        const int Gw = gridDim.x, b = blockIdx.x;
+        const int q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
+        const int t = xcd * q + min(xcd, rr) + (b >> 3);  // XCD-contiguous tiles (guide T1)
+        const int tx = t % ntx, rest = t / ntx;
+        x0 = tx * V_TW;
+        y0 = (rest % nty) * V_TH;
+        n = rest / nty;
+    }
+    const size_t HW = (size_t)H * W;
+    // window of channel block cb: instruction i (wave-strided) fills units [64 i, 64 i + 64)
+    auto dma_win = [&](int cb) __attribute__((always_inline)) {
+        for (int i = wave; i < V_DMA; i += V_NW) {
+            const int pc = (64 * i) / V_PP;
+            const int u = 64 * i - pc * V_PP + lane;
+            const int gl = u / V_GP, r = u - gl * V_GP;
+            const int wr = r / V_RP, wc = r - wr * V_RP;
+            const int iy = y0 - 1 + wr, ix = x0 - 1 + wc;
+            const bool ok = wc < V_WC && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+            const uint32_t off = ok ? (uint32_t)(((size_t)(n * 8 + cb * 4 + gl) * HW + (size_t)iy * W + ix) * 16)
+                                    : 0x80000000u;  // >= num_records -> 0
+            const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(in + (size_t)pc * ips), (short)0, (int)0x80000000u, 0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sm.win + 64 * i), 16, off, 0, 0, 0);
+        }
+    };
+    auto dma_a = [&](int c, int st) __attribute__((always_inline)) {
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(wt + (size_t)c * 12 * 64 * 16), (short)0, (int)0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int row = wave; row < 12; row += V_NW)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sm.a[st] + row * 64), 16,
+                                                     (uint32_t)lane * 16u, row * 64 * 16, 0, 0);
+    };
+    dma_win(0);
+    dma_a(0, 0);
+    dma_a(1, 1);
+    if (tid < 64) sm.b[tid] = bias[tid];
+    // this wave's 32 GEMM columns = pooled row `wave`, pooled cols 4 nb + (q >> 2) for column
+    // blocks nb = 0, 1, quad-major; lane column q = lane & 15, k-group gi = lane >> 4
+    const int q = lane & 15, gi = lane >> 4;
+    const int d = q & 3;
+    const int ty = 2 * wave + (d >> 1);
+    constexpr int PA[6] = {0, 0, 0, 1, 2, 1};
+    constexpr int PB[6] = {2, 0, 1, 0, 0, 1};
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) acc[nb][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    i32x4 fb[2][2][3], fa[2][4][3];
+    auto read_frags = [&](int c, int set) __attribute__((always_inline)) {
+        const int tap = c % 9;
+        const int dy = tap / 3, dx = tap - dy * 3;
+        const uint32_t aw = (uint32_t)(uintptr_t)(lds_ptr_t)(sm.a[c & 1] + gi * 64 + q);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int tx = 2 * (4 * nb + (q >> 2)) + (d & 1);
+            const uint32_t bw = (uint32_t)(uintptr_t)(lds_ptr_t)(sm.win + gi * V_GP + (ty + dy) * V_RP + (tx + dx));
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc)
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[set][nb][pc]) : "v"(bw), "i"(pc * V_PP * 16));
+        }
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc)
+                asm volatile("ds_read_b128 %0, %1 offset:%2"
+                             : "=v"(fa[set][mb][pc])
+                             : "v"(aw), "i"((pc * 4 * 64 + mb * 16) * 16));
+    };
+    auto fence_set = [&](int set) __attribute__((always_inline)) {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) asm volatile("" : "+v"(fb[set][nb][pc]));
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) asm volatile("" : "+v"(fa[set][mb][pc]));
+    };
+    auto mfma_chunk = [&](int set) __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int tt = 0; tt < 6; ++tt)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb)
+                    acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        __builtin_bit_cast(bf16x8, fa[set][mb][PA[tt]]), __builtin_bit_cast(bf16x8, fb[set][nb][PB[tt]]),
+                        acc[nb][mb], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // window block 0, weight chunks 0 and 1
+    __syncthreads();
+    read_frags(0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    fence_set(0);
+    // chunk c's fragments are in register set c & 1 and its weights in stage c & 1; the reads of
+    // chunk c + 1 are issued before chunk c's MFMAs and waited for after them
+#pragma unroll
+    for (int c = 0; c < 18; ++c) {
+        const int set = c & 1;
+        if (c == 8) {
+            // every wave is past chunk 7 (chunk 8's fragments in registers): block 1's window
+            // replaces block 0's and weight chunk 10 goes into chunk 8's stage, behind chunk 8's
+            // MFMAs
+            __syncthreads();
+            dma_win(1);
+            dma_a(10, 0);
+            mfma_chunk(set);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            read_frags(9, set ^ 1);
+        } else {
+            if (c + 1 < 18) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight chunk c + 1 (issued at c - 1)
+                __syncthreads();  // ... landed everywhere; every wave is past chunk c's reads
+                if (c + 2 < 18) dma_a(c + 2, c & 1);
+                read_frags(c + 1, set ^ 1);
+            }
+            mfma_chunk(set);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        fence_set(set ^ 1);
+    }
+    // pooled epilogue: lane holds channels 16 mb + 4 gi + (0..3) of column q of block nb
+    const int Wo = W >> 1, Ho = H >> 1;
+    const size_t HWo = (size_t)Ho * Wo;
+    const int py = (y0 >> 1) + wave;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+        const int px = (x0 >> 1) + 4 * nb + (q >> 2);
+        const bool lead = (lane & 3) == 0 && px < Wo && py < Ho;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            const int m = mb * 16 + 4 * gi;
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float mx = acc[nb][mb][j];
+                mx = fmaxf(mx, __shfl_xor(mx, 1));
+                mx = fmaxf(mx, __shfl_xor(mx, 2));
+                v[j] = fmaxf(mx + sm.b[m + j], 0.f);
+            }
+            if (lead)
+                store4_x6(out + (((size_t)n * 8 + (m >> 3)) * HWo + (size_t)py * Wo + px) * 16 + ((m >> 2) & 1) * 8,
+                          ops, v);
+        }
+    }
+}
+
+void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int W, const uint8_t* wt,
+                              const float* bias, uint8_t* out, uint32_t ops, hipStream_t st) {
+    if (H < 2 || W < 2 || (size_t)N * 8 * H * W * 16 >= 0x80000000ull)
+        throw std::invalid_argument("conv3_pool_win_x6: frame shape out of range");
+    const int tiles = N * ((H + V_TH - 1) / V_TH) * ((W + V_TW - 1) / V_TW);
+    hipLaunchKernelGGL(conv3_pool_win_x6_kernel, dim3(tiles), dim3(64 * V_NW), 0, st, in, ips, N, H, W, wt, bias, out,
+                       ops);
+}
+
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,
                        hipStream_t st) {
     hipLaunchKernelGGL(maxpool_x6_kernel, dim3(grid_for((size_t)NG * (H / 2) * (W / 2))), dim3(256), 0, st, in, ips,

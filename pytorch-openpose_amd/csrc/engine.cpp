@@ -207,6 +207,12 @@ struct opose_ctx {
     // opt-in (OPOSE_CONV12_FUSED=1): bit-identical, but 1.33 ms per bench step against 1.12 ms
     // for the pooled conv1_2 plus a conv1_1 that overlaps the previous step's post kernels
     // (conv_x6.hip)
+    // conv1_2 + pool by conv3_pool_win_x6 (input window in LDS; OPOSE_CONV12_WIN=0: conv_x6's
+    // pooled 64 x 128 tile over the im2col stream)
+    bool win12 = [] {
+        const char* e = getenv("OPOSE_CONV12_WIN");
+        return !(e && e[0] == '0');
+    }();
     bool fused12 = [] {
         const char* e = getenv("OPOSE_CONV12_FUSED");
         return e && e[0] == '1';
@@ -742,6 +748,22 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
         const int og = (s.cout + 7) / 8;
         const size_t np = (size_t)N * hh * ww;
         const bool pooled = s.name == "conv1_2" || s.name == "conv2_2" || s.name == "conv3_4";
+        if (pooled && h->fused_pool && h->win12 && s.name == "conv1_2" && cg == 8 && c->cin == 64 &&
+            c->cout == 64 && c->ks == 3 && c->pad == 1 && c->Mpad == 64 && c->nK6 == 18 && !c->small6) {
+            // conv1_2 + pool with the input window in LDS instead of the 9-tap im2col stream
+            const size_t npo = (size_t)N * (hh / 2) * (ww / 2);
+            ProfEntry pe;
+            h->prof_begin(pe, "conv3x3", 2.0 * 64 * 576 * (double)(npo * 4), 0);
+            if (h->detail) pe.detail = "layer/" + s.name + "/x6win/n" + std::to_string(npo * 4);
+            launch_conv3_pool_win_x6(cur, (uint32_t)(np * 8 * 16), N, hh, ww, c->wx6, c->bias, dst,
+                                     (uint32_t)(npo * 8 * 16), h->stream);
+            h->prof_end(pe);
+            cur = dst;
+            cg = og;
+            hh /= 2;
+            ww /= 2;
+            continue;
+        }
         if (pooled && h->fused_pool) {  // conv + MaxPool2d(2, 2) in one launch
             run_conv_x6(h, c, nullptr, N, hh, ww, x6act(cur, cg, 0, np),
                         x6act(dst, og, 0, (size_t)N * (hh / 2) * (ww / 2)), XAct{}, XAct{}, true, false, XAct{},

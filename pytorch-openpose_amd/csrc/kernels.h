@@ -43,6 +43,9 @@ void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const fl
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,
                        hipStream_t st);
 // conv1_1 + conv1_2 + MaxPool2d(2, 2) fused (x fp32 [N][3][H][W] -> pooled X6 [N][8][H/2 * W/2])
+// conv1_2 (64 -> 64, 3x3 pad 1) + MaxPool2d(2, 2) from an 8-group X6 tensor, input window in LDS
+void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int W, const uint8_t* wt,
+                              const float* bias, uint8_t* out, uint32_t ops, hipStream_t st);
 void launch_conv12_pool_x6(const float* x, int N, int H, int W, const float* w11, int mpad11, const float* b11,
                            const uint8_t* w12, const float* b12, uint8_t* out, uint32_t ops, hipStream_t st);
 

@@ -180,3 +180,38 @@ def test_conv12_fused_bit_identical(native):
             outs.append(y if isinstance(y, tuple) else (y,))
         for a, r in zip(*outs):
             assert np.array_equal(a, r), kind
+
+
+def _model_outputs(cls, kind, x, env):
+    from src import util
+    from src.weights import seeded_state_dict
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        m = cls(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    m.load_state_dict(util.transfer(m, seeded_state_dict(kind, 0)))
+    y = m(x)
+    return y if isinstance(y, tuple) else (y,)
+
+
+@pytest.mark.parametrize("kind,shape", [("body", (2, 3, 72, 104)), ("body", (1, 3, 80, 88)),
+                                        ("body", (1, 3, 184, 328)), ("hand", (1, 3, 88, 88))],
+                         ids=["body72x104", "body80x88", "body184x328", "hand88"])
+def test_conv12_window_bit_identical(native, kind, shape):
+    """conv1_2 + pool with the input window in LDS (conv3_pool_win_x6, default) against conv_x6's
+    pooled launch over the im2col stream (OPOSE_CONV12_WIN=0): the same weight chunks and MFMA
+    sequence per output, so the network outputs are bit-identical.  Partial tiles in the column
+    direction (88 / 104 columns) and the bench's 184 x 328 network input."""
+    from src.model import bodypose_model, handpose_model
+    cls = bodypose_model if kind == "body" else handpose_model
+    x = np.random.default_rng(10).random(shape, dtype=np.float32) - np.float32(0.5)
+    on = _model_outputs(cls, kind, x, {"OPOSE_CONV12_WIN": "1"})
+    off = _model_outputs(cls, kind, x, {"OPOSE_CONV12_WIN": "0"})
+    for a, r in zip(on, off):
+        assert np.array_equal(a, r), kind
