@@ -1174,281 +1174,6 @@ void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const fl
     hipLaunchKernelGGL(conv_first_x6_kernel<3>, dim3(grid), dim3(256), 0, st, x, N, H, W, wt, Mpad, bias, out, ops);
 }
 
-// conv1_1 -> conv1_2 -> MaxPool2d(2, 2) in one launch (src/model.py:37-39 / :141-143; the first
-// three entries of both trunks).  conv1_2 is the M = 64 layer that an implicit GEMM feeds worst:
-// each 16-byte im2col unit serves only 64 output channels, so the separate kernel gathered its
-// 9-tap operand from the 741 MB conv1_1 X6 tensor at half the MFMA rate of the M = 128 layers,
-// after conv1_1 had written that tensor.  Here a workgroup owns an 8 x 16 tile of conv1_2 outputs
-// (4 x 8 pooled pixels) of one frame:
-//  1. conv1_1 for the 10 x 18 window around the tile (conv1_2's zero padding outside the frame),
-//     straight from a 3 x 12 x 20 patch of the fp32 input in LDS: 27 fp32 FMAs per output in
-//     conv_first_x6's order (bit-identical values), bias + ReLU, split into X6 pieces, stored as
-//     the window [piece][channel group][row (pitch 24)][col] in LDS -- the row pitch (== 8 mod
-//     16 units) and group pitch (== 0 mod 16) make every ds_read_b128 lane group below hit 16
-//     distinct bank quads;
-//  2. conv1_2 as 18 k-chunks (2 channel blocks x 9 taps) of the split-bf16 GEMM: weight chunks
-//     by LDS-DMA, two stages, one barrier per chunk; the B fragments are read from the window at
-//     the tap's offset (no im2col traffic at all); 8 waves, each 64 channels x 16 GEMM columns =
-//     4 pooled pixels x their 4 quadrants (quad-major, as the fused-pool epilogue of conv_x6);
-//     the six piece products in conv_x6's MODE 2 order, so the sums are bit-identical to the
-//     separate conv1_1 + pooled conv1_2 launches;
-//  3. 2 x 2 max over the quad's lanes, bias, ReLU, one X6 store per pooled pixel and 4 channels.
-// Opt-in (OPOSE_CONV12_FUSED=1): measured 1.33 ms per bench step (32 frames) against 1.12 ms for
-// the pooled conv1_2 alone, whose conv1_1 (0.16 ms, HBM-store bound) overlaps the previous step's
-// post kernels.  Phase ablations (OPOSE_CONV12_ABL): the chunk loops 0.65 ms (0.61 of the MFMA
-// bound), the conv1_1 window math 0.24 ms, the per-tile skeleton 0.31 ms (splits, barriers, the
-// weight DMA and store latencies of one 139 KB workgroup per CU, which nothing overlaps).  Beating
-// the two-kernel path needs the window of tile t + 1 built while tile t's MFMAs run (producer
-// waves, or two workgroups per CU under 80 KB each), not done.
-namespace {
-constexpr int F_TH = 8, F_TW = 16;                 // conv1_2 outputs per tile
-constexpr int F_WR = F_TH + 2, F_WC = F_TW + 2;    // conv1_1 window 10 x 18
-constexpr int F_RP = 24;                           // window row pitch (units)
-constexpr int F_CGP = F_WR * F_RP;                 // 240 units per channel group
-constexpr int F_PP = 8 * F_CGP;                    // units per piece
-constexpr int F_PR = F_TH + 4, F_PC = F_TW + 4;    // input patch 12 x 20
-constexpr int F_PATCH = 3 * F_PR * F_PC;           // 720 floats
-constexpr int F_PPT = (F_PATCH + 511) / 512;       // patch values per thread
-constexpr int F_NA = 3;                            // weight-chunk stages
-static_assert(F_RP % 16 == 8 && F_CGP % 16 == 0 && F_RP >= F_WC, "conv12 window pitches");
-struct Conv12Smem {
-    uint4 win[3 * F_PP];
-    uint4 a[F_NA][12 * 64];
-    float w11[27 * 64];
-    float b11[64], b12[64];
-    float patch[F_PATCH];
-};
-}  // namespace
-
-// Persistent: one workgroup per CU walks a contiguous range of tiles (XCD-contiguous ranges, guide
-// T1).  Per tile: conv1_1 window (VALU) -> 18 conv1_2 chunks -> pooled stores.  Latency kept off
-// the critical path: the next tile's input patch is loaded into registers while this tile's
-// chunks run; the first two weight chunks of the next tile are DMA'd during this tile's epilogue
-// and window; inside the chunk loop the fragments of chunk c + 1 are read during chunk c's MFMAs
-// (weights three stages deep: the DMA of chunk c + 2 goes into the stage chunk c - 1 used).
-__global__ __launch_bounds__(512, 1) void conv12_pool_x6_kernel(const float* __restrict__ x, int N, int H, int W,
-                                                                const float* __restrict__ w11, int mpad11,
-                                                                const float* __restrict__ b11,
-                                                                const uint8_t* __restrict__ w12,
-                                                                const float* __restrict__ b12,
-                                                                uint8_t* __restrict__ out, uint32_t ops, int abl) {
-    __shared__ Conv12Smem sm;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ntx = (W + F_TW - 1) / F_TW, nty = H / F_TH;
-    const int tiles = N * nty * ntx;
-    int t_lo, t_hi;
-    {
-        const int Gw = gridDim.x, b = blockIdx.x;
-        const int q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
-        const int id = xcd * q + min(xcd, rr) + (b >> 3);
-        t_lo = (int)((long long)id * tiles / Gw);
-        t_hi = (int)((long long)(id + 1) * tiles / Gw);
-    }
-    if (t_lo >= t_hi) return;
-    const size_t HW = (size_t)H * W;
-    auto tile_xy = [&](int t, int& n, int& y0, int& x0) __attribute__((always_inline)) {
-        const int tx = t % ntx, rest = t / ntx;
-        x0 = tx * F_TW;
-        y0 = (rest % nty) * F_TH;
-        n = rest / nty;
-    };
-    // weight chunk c of conv1_2 -> stage st: 12 rows (piece, group) of 64 units, waves w and w + 8
-    auto dma_a = [&](int c, int st) __attribute__((always_inline)) {
-        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(w12 + (size_t)c * 12 * 64 * 16), (short)0, (int)0x7fffffff, 0x00020000);
-        for (int row = wave; row < 12; row += 8)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sm.a[st] + row * 64), 16,
-                                                     (uint32_t)lane * 16u, row * 64 * 16, 0, 0);
-    };
-    auto load_patch = [&](int t, float (&pv)[F_PPT]) __attribute__((always_inline)) {
-        int n, y0, x0;
-        tile_xy(t, n, y0, x0);
-#pragma unroll
-        for (int k = 0; k < F_PPT; ++k) {
-            const int i = tid + 512 * k;
-            const int c = i / (F_PR * F_PC), r = (i / F_PC) % F_PR, cc = i % F_PC;
-            const int iy = y0 - 2 + r, ix = x0 - 2 + cc;
-            const bool ok = i < F_PATCH && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-            pv[k] = ok ? x[((size_t)n * 3 + c) * HW + (size_t)iy * W + ix] : 0.f;
-        }
-    };
-    dma_a(0, 0);
-    dma_a(1, 1);
-    for (int i = tid; i < 27 * 64; i += 512) sm.w11[i] = w11[(size_t)(i >> 6) * mpad11 + (i & 63)];
-    if (tid < 64) {
-        sm.b11[tid] = b11[tid];
-        sm.b12[tid] = b12[tid];
-    }
-    float pv[F_PPT];
-    load_patch(t_lo, pv);
-    // this wave's 16 GEMM columns = pooled row (wave >> 1), pooled cols 4 (wave & 1) .. + 3,
-    // quad-major; lane column q = lane & 15, k-group gi = lane >> 4
-    const int q = lane & 15, gi = lane >> 4;
-    const int prow = wave >> 1, pcol = 4 * (wave & 1) + (q >> 2), d = q & 3;
-    const int ty = 2 * prow + (d >> 1), tx = 2 * pcol + (d & 1);
-    const int Wo = W >> 1, HWo = (H >> 1) * Wo;
-    constexpr int PA[6] = {0, 0, 0, 1, 2, 1};
-    constexpr int PB[6] = {2, 0, 1, 0, 0, 1};
-
-    for (int t = t_lo; t < t_hi; ++t) {
-        int n, y0, x0;
-        tile_xy(t, n, y0, x0);
-#pragma unroll
-        for (int k = 0; k < F_PPT; ++k)
-            if (tid + 512 * k < F_PATCH) sm.patch[tid + 512 * k] = pv[k];
-        __syncthreads();  // patch (and, first tile, w11 / biases) in place; last tile's window reads done
-        // 1. conv1_1 window: item = (window pixel, channel group), consecutive threads along the row
-        for (int it = tid; it < F_WR * F_WC * 8; it += 512) {
-            const int p = it % (F_WR * F_WC), g = it / (F_WR * F_WC);
-            const int wr = p / F_WC, wc = p - wr * F_WC;
-            const int iy = y0 - 1 + wr, ix = x0 - 1 + wc;
-            float v[8];
-            if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W && !(abl & 1)) {
-                float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int k = 0; k < 27; ++k) {
-                    const float in = sm.patch[((k / 9) * F_PR + wr + (k % 9) / 3) * F_PC + wc + k % 3];
-                    const float4 w0 = *reinterpret_cast<const float4*>(sm.w11 + k * 64 + g * 8);
-                    const float4 w1 = *reinterpret_cast<const float4*>(sm.w11 + k * 64 + g * 8 + 4);
-                    acc[0] = __builtin_fmaf(in, w0.x, acc[0]);
-                    acc[1] = __builtin_fmaf(in, w0.y, acc[1]);
-                    acc[2] = __builtin_fmaf(in, w0.z, acc[2]);
-                    acc[3] = __builtin_fmaf(in, w0.w, acc[3]);
-                    acc[4] = __builtin_fmaf(in, w1.x, acc[4]);
-                    acc[5] = __builtin_fmaf(in, w1.y, acc[5]);
-                    acc[6] = __builtin_fmaf(in, w1.z, acc[6]);
-                    acc[7] = __builtin_fmaf(in, w1.w, acc[7]);
-                }
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = fmaxf(acc[j] + sm.b11[g * 8 + j], 0.f);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = 0.f;  // conv1_2's zero padding
-            }
-            uint32_t hp[3][8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) split3(v[j], hp[0][j], hp[1][j], hp[2][j]);
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) {
-                uint4 w4;
-                w4.x = hp[pc][0] | (hp[pc][1] << 16);
-                w4.y = hp[pc][2] | (hp[pc][3] << 16);
-                w4.z = hp[pc][4] | (hp[pc][5] << 16);
-                w4.w = hp[pc][6] | (hp[pc][7] << 16);
-                if (!(abl & 8)) sm.win[pc * F_PP + g * F_CGP + wr * F_RP + wc] = w4;
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight chunks 0 and 1 of this tile
-        __syncthreads();  // window written; chunks 0, 1 landed everywhere
-        // 2. conv1_2 chunks; fragment set c & 1 holds chunk c.  The reads of chunk c + 1 are
-        //    issued (inline asm, so the compiler cannot sink them to their uses) before chunk c's
-        //    24 MFMAs and waited for after them: the LDS latency hides behind the MFMAs
-        f32x4 acc[4];
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-        i32x4 fb[2][3], fa[2][4][3];
-        auto read_frags = [&](int c, int set) __attribute__((always_inline)) {
-            const int cb = c / 9, tap = c - cb * 9;
-            const int dy = tap / 3, dx = tap - dy * 3;
-            const uint32_t bw = (uint32_t)(uintptr_t)(lds_ptr_t)(sm.win + (cb * 4 + gi) * F_CGP + (ty + dy) * F_RP +
-                                                                 (tx + dx));
-            const uint32_t aw = (uint32_t)(uintptr_t)(lds_ptr_t)(sm.a[c % F_NA] + gi * 64 + q);
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc)
-                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[set][pc]) : "v"(bw), "i"(pc * F_PP * 16));
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-                for (int pc = 0; pc < 3; ++pc)
-                    asm volatile("ds_read_b128 %0, %1 offset:%2"
-                                 : "=v"(fa[set][mb][pc])
-                                 : "v"(aw), "i"((pc * 4 * 64 + mb * 16) * 16));
-        };
-        auto fence_set = [&](int set) __attribute__((always_inline)) {
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) asm volatile("" : "+v"(fb[set][pc]));
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-                for (int pc = 0; pc < 3; ++pc) asm volatile("" : "+v"(fa[set][mb][pc]));
-        };
-        read_frags(0, 0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        fence_set(0);
-        const int nc = (abl & 2) ? 0 : 18;
-#pragma unroll 2
-        for (int c = 0; c < nc; ++c) {
-            const int set = c & 1;
-            if (c + 1 < 18) {
-                if (c >= 1) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // DMA of chunk c + 1 (issued at c - 1)
-                    __syncthreads();  // ... landed everywhere; every wave is past chunk c - 1's reads
-                }
-                if (c + 2 < 18) dma_a(c + 2, (c + 2) % F_NA);  // stage of chunk c - 1
-                read_frags(c + 1, set ^ 1);
-                // the next tile's input patch: after the last weight wait of this tile (vmcnt is
-                // in order), consumed at the next tile's start
-                if (c == 16 && t + 1 < t_hi) load_patch(t + 1, pv);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int tt = 0; tt < 6; ++tt)
-#pragma unroll
-                for (int mb = 0; mb < 4; ++mb)
-                    acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[set][mb][PA[tt]]),
-                                                                      __builtin_bit_cast(bf16x8, fb[set][PB[tt]]),
-                                                                      acc[mb], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            fence_set(set ^ 1);
-        }
-        __syncthreads();  // every wave is done with the weight stages and the window
-        if (t + 1 < t_hi) {  // the next tile's first two chunks, behind the epilogue and its window
-            dma_a(0, 0);
-            dma_a(1, 1);
-        }
-        // 3. pooled epilogue: lane holds channels 16 mb + 4 gi + (0..3) of column q
-        const int py = (y0 >> 1) + prow, px = (x0 >> 1) + pcol;
-        const bool lead = (lane & 3) == 0 && px < Wo;
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) {
-            const int m = mb * 16 + 4 * gi;
-            float v[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                float mx = acc[mb][j];
-                mx = fmaxf(mx, __shfl_xor(mx, 1));
-                mx = fmaxf(mx, __shfl_xor(mx, 2));
-                v[j] = fmaxf(mx + sm.b12[m + j], 0.f);
-            }
-            if (lead && !(abl & 4))
-                store4_x6(out + (((size_t)n * 8 + (m >> 3)) * HWo + (size_t)py * Wo + px) * 16 + ((m >> 2) & 1) * 8,
-                          ops, v);
-        }
-    }
-}
-
-void launch_conv12_pool_x6(const float* x, int N, int H, int W, const float* w11, int mpad11, const float* b11,
-                           const uint8_t* w12, const float* b12, uint8_t* out, uint32_t ops, hipStream_t st) {
-    if (H % F_TH || W % 2) throw std::invalid_argument("conv12_pool_x6: H must be a multiple of 8, W even");
-    static const int abl = [] {  // timing ablations (results wrong): 1 no conv1_1 math, 2 no conv1_2 loop, 4 no
-        // output stores, 8 no window LDS stores
-        const char* e = getenv("OPOSE_CONV12_ABL");
-        return e ? atoi(e) : 0;
-    }();
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        OPOSE_HIP_CHECK(hipGetDevice(&dev));
-        OPOSE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    const int tiles = N * (H / F_TH) * ((W + F_TW - 1) / F_TW);
-    const int grid = tiles < cus ? tiles : cus;  // persistent: one workgroup per CU (127 KB of LDS)
-    hipLaunchKernelGGL(conv12_pool_x6_kernel, dim3(grid), dim3(512), 0, st, x, N, H, W, w11, mpad11, b11, w12, b12,
-                       out, ops, abl);
-}
-
 // ---------------------------------------------------------------- windowed conv1_2 (+ pool)
 // conv1_2 (64 -> 64 channels, 3x3, pad 1) + MaxPool2d(2, 2) from conv1_1's X6 tensor, with the
 // im2col operand replaced by a window (src/model.py:35-37 / :145-147).  conv_x6 streams each
@@ -1458,8 +1183,8 @@ void launch_conv12_pool_x6(const float* x, int N, int H, int W, const float* w11
 // channel block (4 groups = 32 channels), DMAs the 10 x 18 input window once (69 KB per tile for
 // both blocks) and reads the nine taps' B fragments from it at the tap's offset:
 //  * window [piece][group][row (pitch 24 units)][col]: the pitch (== 8 mod 16 units) and the
-//    group pitch (== 0 mod 16) put every ds_read_b128 lane group on 16 distinct bank quads (as
-//    conv12_pool_x6); the pad columns 18..23 and the frame border load zeros through the buffer
+//    group pitch (== 0 mod 16) put every ds_read_b128 lane group on 16 distinct bank quads;
+//    the pad columns 18..23 and the frame border load zeros through the buffer
 //    range check (conv1_2's zero padding);
 //  * 18 k-chunks (2 channel blocks x 9 taps) in the weight layout of conv_x6 (one chunk = 12
 //    (piece, group) rows of 64 units), two weight stages by LDS-DMA, one barrier per chunk;
@@ -1657,6 +1382,250 @@ void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int
     const int tiles = N * ((H + V_TH - 1) / V_TH) * ((W + V_TW - 1) / V_TW);
     hipLaunchKernelGGL(conv3_pool_win_x6_kernel, dim3(tiles), dim3(64 * V_NW), 0, st, in, ips, N, H, W, wt, bias, out,
                        ops);
+}
+
+// ---------------------------------------------------------------- conv1_1 + conv1_2 (+ pool), windowed
+// conv3_pool_win_x6 with its window computed instead of loaded: per channel block, conv1_1
+// (src/model.py:35 / :145, 3 -> 64 channels) for the 10 x 18 window around the tile straight from
+// a 3 x 12 x 20 patch of the fp32 input in LDS -- 27 fp32 FMAs per output in conv_first_x6's order,
+// bias, ReLU, split into the X6 pieces -- so conv1_1's 64-channel full-resolution tensor (741 MB
+// written and read back per bench step) never exists.  Everything after the window is
+// conv3_pool_win_x6's: bit-identical to conv_first_x6 + the pooled conv1_2.  Block 1's window is
+// built while chunk 8's MFMAs run.  78 KB of LDS: conv1_1's weights are staged per channel block.
+// Opt-in (OPOSE_CONV12_FUSED=1): it ties with the two launches it replaces -- 0.86 vs 0.17 + 0.66
+// ms serial, 1.32 vs 0.34 + 0.93 ms beside the previous step's post kernels (scripts/conv12_ab.sh).
+// The window math (1.4x the conv1_1 outputs, halo included, plus the splits) costs as much VALU
+// time as the 741 MB store and re-read it saves; the two workgroups of a CU run their window
+// phases at the same time rather than under each other's MFMAs.
+namespace {
+constexpr int V_PR = V_TH + 4, V_PC = V_TW + 4;    // input patch 12 x 20
+constexpr int V_PATCH = 3 * V_PR * V_PC;           // 720 floats
+struct Win12Smem {
+    uint4 win[V_WIN];
+    uint4 a[2][12 * 64];
+    float w11[27 * 32];  // conv1_1 weights of one channel block: [k][32]
+    float b11[64], b12[64];
+    float patch[V_PATCH];
+};
+}  // namespace
+
+__global__ __launch_bounds__(256, 2) void conv12_pool_win_x6_kernel(const float* __restrict__ x, int N, int H, int W,
+                                                                    const float* __restrict__ w11, int mpad11,
+                                                                    const float* __restrict__ b11,
+                                                                    const uint8_t* __restrict__ wt,
+                                                                    const float* __restrict__ b12,
+                                                                    uint8_t* __restrict__ out, uint32_t ops) {
+    __shared__ Win12Smem sm;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ntx = (W + V_TW - 1) / V_TW, nty = (H + V_TH - 1) / V_TH;
+    int n, y0, x0;
+    {
+        const int Gw = gridDim.x, b = blockIdx.x;
+        const int q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
+        const int t = xcd * q + min(xcd, rr) + (b >> 3);  // XCD-contiguous tiles (guide T1)
+        const int tx = t % ntx, rest = t / ntx;
+        x0 = tx * V_TW;
+        y0 = (rest % nty) * V_TH;
+        n = rest / nty;
+    }
+    const size_t HW = (size_t)H * W;
+    auto dma_a = [&](int c, int st) __attribute__((always_inline)) {
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(wt + (size_t)c * 12 * 64 * 16), (short)0, (int)0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int row = wave; row < 12; row += V_NW)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sm.a[st] + row * 64), 16,
+                                                     (uint32_t)lane * 16u, row * 64 * 16, 0, 0);
+    };
+    auto load_w11 = [&](int cb) __attribute__((always_inline)) {
+        for (int i = tid; i < 27 * 32; i += 64 * V_NW) sm.w11[i] = w11[(size_t)(i >> 5) * mpad11 + cb * 32 + (i & 31)];
+    };
+    // conv1_1 window of channel block cb: item = (window pixel, group), consecutive threads along
+    // the row; pixels outside the frame are conv1_2's zero padding
+    auto build_window = [&](int cb) __attribute__((always_inline)) {
+        for (int it = tid; it < V_WR * V_WC * 4; it += 64 * V_NW) {
+            const int p = it % (V_WR * V_WC), gl = it / (V_WR * V_WC);
+            const int wr = p / V_WC, wc = p - wr * V_WC;
+            const int iy = y0 - 1 + wr, ix = x0 - 1 + wc;
+            float v[8];
+            if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {
+                float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < 27; ++k) {
+                    const float in = sm.patch[((k / 9) * V_PR + wr + (k % 9) / 3) * V_PC + wc + k % 3];
+                    const float4 w0 = *reinterpret_cast<const float4*>(sm.w11 + k * 32 + gl * 8);
+                    const float4 w1 = *reinterpret_cast<const float4*>(sm.w11 + k * 32 + gl * 8 + 4);
+                    acc[0] = __builtin_fmaf(in, w0.x, acc[0]);
+                    acc[1] = __builtin_fmaf(in, w0.y, acc[1]);
+                    acc[2] = __builtin_fmaf(in, w0.z, acc[2]);
+                    acc[3] = __builtin_fmaf(in, w0.w, acc[3]);
+                    acc[4] = __builtin_fmaf(in, w1.x, acc[4]);
+                    acc[5] = __builtin_fmaf(in, w1.y, acc[5]);
+                    acc[6] = __builtin_fmaf(in, w1.z, acc[6]);
+                    acc[7] = __builtin_fmaf(in, w1.w, acc[7]);
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = fmaxf(acc[j] + sm.b11[cb * 32 + gl * 8 + j], 0.f);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = 0.f;
+            }
+            uint32_t hp[3][8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) split3(v[j], hp[0][j], hp[1][j], hp[2][j]);
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) {
+                uint4 w4;
+                w4.x = hp[pc][0] | (hp[pc][1] << 16);
+                w4.y = hp[pc][2] | (hp[pc][3] << 16);
+                w4.z = hp[pc][4] | (hp[pc][5] << 16);
+                w4.w = hp[pc][6] | (hp[pc][7] << 16);
+                sm.win[pc * V_PP + gl * V_GP + wr * V_RP + wc] = w4;
+            }
+        }
+    };
+    dma_a(0, 0);
+    dma_a(1, 1);
+    for (int i = tid; i < V_PATCH; i += 64 * V_NW) {
+        const int c = i / (V_PR * V_PC), r = (i / V_PC) % V_PR, cc = i % V_PC;
+        const int iy = y0 - 2 + r, ix = x0 - 2 + cc;
+        const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        sm.patch[i] = ok ? x[((size_t)n * 3 + c) * HW + (size_t)iy * W + ix] : 0.f;
+    }
+    load_w11(0);
+    if (tid < 64) {
+        sm.b11[tid] = b11[tid];
+        sm.b12[tid] = b12[tid];
+    }
+    __syncthreads();
+    build_window(0);
+    __syncthreads();  // window 0 complete; conv1_1's block-0 weights free
+    load_w11(1);      // read at chunk 8, after several barriers
+    // this wave's 32 GEMM columns = pooled row `wave`, pooled cols 4 nb + (q >> 2) for column
+    // blocks nb = 0, 1, quad-major; lane column q = lane & 15, k-group gi = lane >> 4
+    const int q = lane & 15, gi = lane >> 4;
+    const int d = q & 3;
+    const int ty = 2 * wave + (d >> 1);
+    constexpr int PA[6] = {0, 0, 0, 1, 2, 1};
+    constexpr int PB[6] = {2, 0, 1, 0, 0, 1};
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) acc[nb][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    i32x4 fb[2][2][3], fa[2][4][3];
+    auto read_frags = [&](int c, int set) __attribute__((always_inline)) {
+        const int tap = c % 9;
+        const int dy = tap / 3, dx = tap - dy * 3;
+        const uint32_t aw = (uint32_t)(uintptr_t)(lds_ptr_t)(sm.a[c & 1] + gi * 64 + q);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int tx = 2 * (4 * nb + (q >> 2)) + (d & 1);
+            const uint32_t bw = (uint32_t)(uintptr_t)(lds_ptr_t)(sm.win + gi * V_GP + (ty + dy) * V_RP + (tx + dx));
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc)
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[set][nb][pc]) : "v"(bw), "i"(pc * V_PP * 16));
+        }
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc)
+                asm volatile("ds_read_b128 %0, %1 offset:%2"
+                             : "=v"(fa[set][mb][pc])
+                             : "v"(aw), "i"((pc * 4 * 64 + mb * 16) * 16));
+    };
+    auto fence_set = [&](int set) __attribute__((always_inline)) {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) asm volatile("" : "+v"(fb[set][nb][pc]));
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int pc = 0; pc < 3; ++pc) asm volatile("" : "+v"(fa[set][mb][pc]));
+    };
+    auto mfma_chunk = [&](int set) __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int tt = 0; tt < 6; ++tt)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb)
+                    acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        __builtin_bit_cast(bf16x8, fa[set][mb][PA[tt]]), __builtin_bit_cast(bf16x8, fb[set][nb][PB[tt]]),
+                        acc[nb][mb], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight chunks 0 and 1
+    __syncthreads();
+    read_frags(0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    fence_set(0);
+    auto step = [&](int c) __attribute__((always_inline)) {  // chunk c != 8
+        const int set = c & 1;
+        if (c + 1 < 18) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight chunk c + 1 (issued at c - 1)
+            __syncthreads();  // ... landed everywhere; every wave is past chunk c's reads
+            if (c + 2 < 18) dma_a(c + 2, c & 1);
+            read_frags(c + 1, set ^ 1);
+        }
+        mfma_chunk(set);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        fence_set(set ^ 1);
+    };
+    // (three loops, so that the window build stays out of the unrolled chunk loops: the register
+    // sets are indexed by the unrolled chunk number)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) step(c);
+    {
+        // every wave is past chunk 7 (chunk 8's fragments in registers, set 0): block 1's window
+        // is built over block 0's while chunk 8's MFMAs run; weight chunk 10 into chunk 8's stage
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight chunk 9 (issued at chunk 7)
+        __syncthreads();
+        dma_a(10, 0);
+        mfma_chunk(0);
+        build_window(1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        read_frags(9, 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        fence_set(1);
+    }
+#pragma unroll
+    for (int c = 9; c < 18; ++c) step(c);
+    const int Wo = W >> 1, Ho = H >> 1;
+    const size_t HWo = (size_t)Ho * Wo;
+    const int py = (y0 >> 1) + wave;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+        const int px = (x0 >> 1) + 4 * nb + (q >> 2);
+        const bool lead = (lane & 3) == 0 && px < Wo && py < Ho;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            const int m = mb * 16 + 4 * gi;
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float mx = acc[nb][mb][j];
+                mx = fmaxf(mx, __shfl_xor(mx, 1));
+                mx = fmaxf(mx, __shfl_xor(mx, 2));
+                v[j] = fmaxf(mx + sm.b12[m + j], 0.f);
+            }
+            if (lead)
+                store4_x6(out + (((size_t)n * 8 + (m >> 3)) * HWo + (size_t)py * Wo + px) * 16 + ((m >> 2) & 1) * 8,
+                          ops, v);
+        }
+    }
+}
+
+void launch_conv12_pool_win_x6(const float* x, int N, int H, int W, const float* w11, int mpad11, const float* b11,
+                               const uint8_t* w12, const float* b12, uint8_t* out, uint32_t ops, hipStream_t st) {
+    if (H < 2 || W < 2 || mpad11 < 64) throw std::invalid_argument("conv12_pool_win_x6: shape out of range");
+    const int tiles = N * ((H + V_TH - 1) / V_TH) * ((W + V_TW - 1) / V_TW);
+    hipLaunchKernelGGL(conv12_pool_win_x6_kernel, dim3(tiles), dim3(64 * V_NW), 0, st, x, N, H, W, w11, mpad11, b11,
+                       w12, b12, out, ops);
 }
 
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,

@@ -203,19 +203,18 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_FIRST_DIRECT");
         return !(e && e[0] == '0');
     }();
-    // conv1_1 + conv1_2 + pool in one launch (conv12_pool_x6; needs first_direct and fused_pool),
-    // opt-in (OPOSE_CONV12_FUSED=1): bit-identical, but 1.33 ms per bench step against 1.12 ms
-    // for the pooled conv1_2 plus a conv1_1 that overlaps the previous step's post kernels
-    // (conv_x6.hip)
+    // conv1_1 + conv1_2 + pool in one launch (conv12_pool_win_x6; needs first_direct and
+    // fused_pool), opt-in (OPOSE_CONV12_FUSED=1): bit-identical, and a tie with conv_first_x6 +
+    // conv3_pool_win_x6 (conv_x6.hip)
+    bool fused12 = [] {
+        const char* e = getenv("OPOSE_CONV12_FUSED");
+        return e && e[0] == '1';
+    }();
     // conv1_2 + pool by conv3_pool_win_x6 (input window in LDS; OPOSE_CONV12_WIN=0: conv_x6's
     // pooled 64 x 128 tile over the im2col stream)
     bool win12 = [] {
         const char* e = getenv("OPOSE_CONV12_WIN");
         return !(e && e[0] == '0');
-    }();
-    bool fused12 = [] {
-        const char* e = getenv("OPOSE_CONV12_FUSED");
-        return e && e[0] == '1';
     }();
     // single-scale Body: the heat-map resize fused into the NMS tiles (gauss_nms_resize, post.hip),
     // opt-in (OPOSE_FUSE_HEAT=1): bit-identical, but 1.10 ms per bench step against 0.47 + 0.43 ms
@@ -713,7 +712,7 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
                 ProfEntry pe;
                 h->prof_begin(pe, "conv3x3", 2.0 * 64 * (27 + 576) * (double)npix, 0);
                 if (h->detail) pe.detail = "layer/conv1_1+conv1_2+pool/fused/n" + std::to_string(npix);
-                launch_conv12_pool_x6(x, N, H, W, c->wt, c->Mpad, c->bias, c2->wx6, c2->bias, A,
+                launch_conv12_pool_win_x6(x, N, H, W, c->wt, c->Mpad, c->bias, c2->wx6, c2->bias, A,
                                       (uint32_t)(npo * 8 * 16), h->stream);
                 h->prof_end(pe);
                 cur = A;

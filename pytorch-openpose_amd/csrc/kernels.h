@@ -46,9 +46,10 @@ void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t o
 // conv1_2 (64 -> 64, 3x3 pad 1) + MaxPool2d(2, 2) from an 8-group X6 tensor, input window in LDS
 void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int W, const uint8_t* wt,
                               const float* bias, uint8_t* out, uint32_t ops, hipStream_t st);
-void launch_conv12_pool_x6(const float* x, int N, int H, int W, const float* w11, int mpad11, const float* b11,
-                           const uint8_t* w12, const float* b12, uint8_t* out, uint32_t ops, hipStream_t st);
-
+// conv1_1 + conv1_2 + pool, the conv1_1 window computed per channel block in LDS (no 64-channel
+// full-resolution tensor)
+void launch_conv12_pool_win_x6(const float* x, int N, int H, int W, const float* w11, int mpad11, const float* b11,
+                               const uint8_t* w12, const float* b12, uint8_t* out, uint32_t ops, hipStream_t st);
 // imgproc.hip
 void launch_preprocess(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int Hs,
                        int Ws, double sy, double sx, int Hp, int Wp, float pad_val, float* out, hipStream_t st);

@@ -154,8 +154,8 @@ def test_network_variants(native, env):
 
 
 def test_conv12_fused_bit_identical(native):
-    """conv1_1 + conv1_2 + MaxPool2d in one launch (conv12_pool_x6, opt-in OPOSE_CONV12_FUSED=1)
-    against the separate conv_first_x6 and pooled conv_x6 launches (default): the same fp32 FMA order for
+    """conv1_1 + conv1_2 + MaxPool2d in one launch (conv12_pool_win_x6, opt-in OPOSE_CONV12_FUSED=1)
+    against the separate conv_first_x6 and windowed conv1_2 launches (default): the same fp32 FMA order for
     conv1_1 and the same MFMA sequence per output, so the network outputs are bit-identical.
     Shapes with a partial 16-column tile (104 / 88 columns) and several frames."""
     from src import util
