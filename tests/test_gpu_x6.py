@@ -201,8 +201,11 @@ def _model_outputs(cls, kind, x, env):
 
 
 @pytest.mark.parametrize("kind,shape", [("body", (2, 3, 72, 104)), ("body", (1, 3, 80, 88)),
-                                        ("body", (1, 3, 184, 328)), ("hand", (1, 3, 88, 88))],
-                         ids=["body72x104", "body80x88", "body184x328", "hand88"])
+                                        ("body", (1, 3, 184, 328)), ("hand", (1, 3, 88, 88)),
+                                        ("body", (3, 3, 8, 8)), ("body", (1, 3, 16, 120)),
+                                        ("hand", (2, 3, 40, 24)), ("hand", (1, 3, 56, 200))],
+                         ids=["body72x104", "body80x88", "body184x328", "hand88", "body3x8x8", "body16x120",
+                              "hand2x40x24", "hand56x200"])
 def test_conv12_window_bit_identical(native, kind, shape):
     """conv1_2 + pool with the input window in LDS (conv3_pool_win_x6, default) against conv_x6's
     pooled launch over the im2col stream (OPOSE_CONV12_WIN=0): the same weight chunks and MFMA
