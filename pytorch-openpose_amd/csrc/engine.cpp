@@ -381,7 +381,17 @@ TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false)
     // 64x256 = four 64x64 waves for the M = 64 layers, opt-in (OPOSE_X6_T64X256=1): conv1_2
     // measured 91 vs 109 TF/s with 64x128 -- an M = 64 tile loads the same im2col bytes per MFMA
     // whatever its width, and one workgroup per CU leaves one wave per SIMD (scripts/t64_ab.sh)
-    static const double ovh6[7] = {1.5, 1.0, 0.96, 1.1, 1.1, 1.2, 1.0};
+    static const double ovh6_big[7] = {1.5, 1.0, 0.96, 1.1, 1.1, 1.2, 1.0};
+    // layers of one or two small frames (C2 / C3 / single-frame C5, stream-K over the whole chip):
+    // 128x128 priced like the 8-wave tiles and 64x64 higher -- measured, C2 1.91 -> 1.72 ms and
+    // Hand() 10.0 -> 9.9 ms, C5 and the bench unchanged; the same weights on the bench's
+    // 32-frame layers cost 6 % (scripts/c2_tile_ab.sh; OPOSE_X6_SMALL_OVH=0 disables)
+    static const double ovh6_small[7] = {1.0, 1.0, 0.96, 1.1, 1.1, 1.6, 1.0};
+    static const bool small_ovh = [] {
+        const char* e = getenv("OPOSE_X6_SMALL_OVH");
+        return !(e && e[0] == '0');
+    }();
+    const double* ovh6 = small_ovh && (long)npix * ngroups <= 16384 ? ovh6_small : ovh6_big;
     static const bool t64x256 = [] {
         const char* e = getenv("OPOSE_X6_T64X256");
         return e && e[0] == '1';
