@@ -372,7 +372,7 @@ struct TileChoice {
 // holds k >= 2 co-resident workgroups finishes them in k * work; a lone workgroup (one wave per
 // SIMD) runs at ~60 %.  Stream-K (grid = all resident slots) balances the chip exactly and
 // pays for the partial slabs of tiles it splits plus one fixup launch.
-TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false) {
+TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false, bool dp_only = false) {
     static const int cfg[7][3] = {{128, 128, 2}, {128, 256, 1}, {256, 128, 1}, {128, 64, 3},
                                   {64, 128, 3},  {64, 64, 4},   {64, 256, 0}};  // mt, pt, WG/CU
     // split-bf16 kernel: 2.5x the MFMA rate per chunk, more LDS per workgroup
@@ -426,7 +426,7 @@ TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false)
         // stream-K over every resident slot (each workgroup >= 4 chunks)
         const long iters = tiles * nK;
         long grid = std::min<long>(256L * occ, iters / 4);
-        if (grid >= 1 && grid != tiles) {
+        if (!dp_only && grid >= 1 && grid != tiles) {
             const double per_wg = (double)iters / grid;
             const double cu_load = std::max(floor1, std::ceil(grid / 256.0)) * per_wg * unit;
             // partial slabs: every workgroup segment that is not a whole tile writes one, the
@@ -683,8 +683,9 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
         a.g[0].out2_off = dup.off;
     }
     if (ng == 1) a.g[1] = a.g[0];
-    TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.nK, true);
-    if (pool) t.grid = (a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * ng;  // whole tiles (data parallel)
+    // pooled convs run whole tiles (data parallel): price only those
+    TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.nK, true, pool);
+    if (pool) t.grid = (a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * ng;
     a.ngroups = ng;
     a.sk_grid = t.grid;
     a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
