@@ -511,57 +511,72 @@ __global__ __launch_bounds__(256) void blur5_seed(const float* __restrict__ heat
     if (threadIdx.x == 0 && s_n) atomicAdd(cnt + np, s_n);
 }
 
-// One workgroup per frame: order each part's peaks row-major (np.nonzero), assign the
-// global running ids, write candidate rows (x, y, score, id) into the record.
-__global__ __launch_bounds__(256) void peaks_finalize(const int* __restrict__ cnt, const int* __restrict__ list,
+// One workgroup per (frame, part): order the part's peaks row-major (np.nonzero), assign the
+// global running ids (the counts of the parts before it), write candidate rows (x, y, score, id)
+// into the record.  (One workgroup per frame walking the 18 parts took 40 us for a single frame:
+// 18 dependent global round trips.)
+__global__ __launch_bounds__(128) void peaks_finalize(const int* __restrict__ cnt, const int* __restrict__ list,
                                                       const double* __restrict__ list_score, int H, int W, RecordLayout L,
                                                       uint8_t* __restrict__ records, int* __restrict__ peak_pos,
                                                       int* __restrict__ part_cnt) {
-    const int n = blockIdx.x;
+    const int n = blockIdx.x / 18, p = blockIdx.x - n * 18;
     const int cap = L.peaks_per_part;
-    __shared__ int s_cnt[18], s_start[18];
-    if (threadIdx.x == 0) {
-        int acc = 0, over = 0;
-        for (int p = 0; p < 18; ++p) {
-            int c = cnt[n * 18 + p];
-            if (c > cap) {
-                over = 1;
-                c = cap;
-            }
-            s_cnt[p] = c;
-            s_start[p] = acc;
-            acc += c;
+    __shared__ int s_c, s_start;
+    __shared__ int s_v[1024];
+    if (threadIdx.x < 64) {  // one wave: clamped counts, this part's start, the header (part 0)
+        const int q = threadIdx.x;
+        const int raw = q < 18 ? cnt[n * 18 + q] : 0;
+        const int c = raw > cap ? cap : raw;
+        int before = q < p ? c : 0;
+        int total = c;
+        bool over = raw > cap;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            before += __shfl_xor(before, off);
+            total += __shfl_xor(total, off);
         }
-        int32_t* hdr = reinterpret_cast<int32_t*>(records + (size_t)n * L.bytes);
-        hdr[0] = over ? -5 : 0;
-        hdr[1] = acc;
-        hdr[2] = 0;
-        hdr[3] = 0;
+        const bool any_over = __ballot(over) != 0ull;
+        if (q == p) s_c = c;
+        if (q == 0) {
+            s_start = before;
+            if (p == 0) {
+                int32_t* hdr = reinterpret_cast<int32_t*>(records + (size_t)n * L.bytes);
+                hdr[0] = any_over ? -5 : 0;
+                hdr[1] = total;
+                hdr[2] = 0;
+                hdr[3] = 0;
+            }
+        }
     }
     __syncthreads();
+    const int c = s_c;
+    const int* lp = list + ((size_t)n * 18 + p) * cap;
+    const bool staged = c <= 1024;
+    if (staged)
+        for (int i = threadIdx.x; i < c; i += blockDim.x) s_v[i] = lp[i];
+    __syncthreads();
     double* cand = reinterpret_cast<double*>(records + (size_t)n * L.bytes + L.cand_off);
-    for (int p = 0; p < 18; ++p) {
-        const int c = s_cnt[p];
-        const int* lp = list + ((size_t)n * 18 + p) * cap;
-        for (int i = threadIdx.x; i < c; i += blockDim.x) {
-            const int v = lp[i];
-            int rank = 0;
-            for (int j = 0; j < c; ++j) rank += lp[j] < v;
-            const int y = v / W, x = v - y * W;
-            const int id = s_start[p] + rank;
-            double* row = cand + (size_t)id * 4;
-            row[0] = (double)x;
-            row[1] = (double)y;
-            row[2] = list_score[((size_t)n * 18 + p) * cap + i];
-            row[3] = (double)id;
-            peak_pos[((size_t)n * 18 + p) * cap + rank] = v;
-        }
-        if (threadIdx.x == 0) part_cnt[n * 18 + p] = c;
+    for (int i = threadIdx.x; i < c; i += blockDim.x) {
+        const int v = staged ? s_v[i] : lp[i];
+        int rank = 0;
+        for (int j = 0; j < c; ++j) rank += (staged ? s_v[j] : lp[j]) < v;
+        const int y = v / W, x = v - y * W;
+        const int id = s_start + rank;
+        double* row = cand + (size_t)id * 4;
+        row[0] = (double)x;
+        row[1] = (double)y;
+        row[2] = list_score[((size_t)n * 18 + p) * cap + i];
+        row[3] = (double)id;
+        peak_pos[((size_t)n * 18 + p) * cap + rank] = v;
     }
+    if (threadIdx.x == 0) part_cnt[n * 18 + p] = c;
 }
 
 // grid (frames * 19 limbs, blocks per limb); pair (i, j) -> score[n][k][i*nB + j]
-// (-inf when criterion1/criterion2 fail; src/body.py:137-141).
+// (-inf when criterion1/criterion2 fail; src/body.py:137-141).  A thread per (pair, sample): the
+// ten samples of a pair are evaluated by ten lanes (each a cubic resample chain of dependent
+// loads), then summed in sample order by the pair's first lane -- the reference's float64 order.
+constexpr int PS_PAIRS = 25;  // pairs per 256-thread pass (250 lanes)
 __global__ __launch_bounds__(256) void paf_score(PafScales S, const int* __restrict__ peak_pos,
                                                  const int* __restrict__ part_cnt, int cap, double thre2,
                                                  double* __restrict__ score) {
@@ -574,19 +589,23 @@ __global__ __launch_bounds__(256) void paf_score(PafScales S, const int* __restr
     const int* posA = peak_pos + ((size_t)n * 18 + pa) * cap;
     const int* posB = peak_pos + ((size_t)n * 18 + pb) * cap;
     double* out = score + (size_t)nk * cap * cap;
-    for (int e = blockIdx.y * blockDim.x + threadIdx.x; e < total; e += gridDim.y * blockDim.x) {
-        const int i = e / nB, j = e - i * nB;
-        const int va = posA[i], vb = posB[j];
-        const int ya = va / S.W, xa = va - ya * S.W;
-        const int yb = vb / S.W, xb = vb - yb * S.W;
-        const long long vx = xb - xa, vy = yb - ya;
-        const double norm = sqrt((double)(vx * vx + vy * vy)) + 1e-10;
-        const double ux = (double)vx / norm, uy = (double)vy / norm;
-        const double stx = ((double)xb - (double)xa) / 9.0;
-        const double sty = ((double)yb - (double)ya) / 9.0;
-        double acc = 0.0;
-        int above = 0;
-        for (int t = 0; t < 10; ++t) {
+    __shared__ double s_sm[PS_PAIRS * 10];
+    const int q = threadIdx.x / 10, t = threadIdx.x - q * 10;  // pair slot, sample
+    for (int e0 = blockIdx.y * PS_PAIRS; e0 < total; e0 += gridDim.y * PS_PAIRS) {
+        const int e = e0 + q;
+        const bool live = q < PS_PAIRS && e < total;
+        double ux = 0.0, uy = 0.0, norm = 1.0;
+        if (live) {
+            const int i = e / nB, j = e - i * nB;
+            const int va = posA[i], vb = posB[j];
+            const int ya = va / S.W, xa = va - ya * S.W;
+            const int yb = vb / S.W, xb = vb - yb * S.W;
+            const long long vx = xb - xa, vy = yb - ya;
+            norm = sqrt((double)(vx * vx + vy * vy)) + 1e-10;
+            ux = (double)vx / norm;
+            uy = (double)vy / norm;
+            const double stx = ((double)xb - (double)xa) / 9.0;
+            const double sty = ((double)yb - (double)ya) / 9.0;
             const double fx = t == 9 ? (double)xb : (double)t * stx + (double)xa;
             const double fy = t == 9 ? (double)yb : (double)t * sty + (double)ya;
             const int X = (int)rint(fx), Y = (int)rint(fy);
@@ -610,13 +629,22 @@ __global__ __launch_bounds__(256) void paf_score(PafScales S, const int* __restr
                 px = px + (double)(vx_ / (float)S.n);
                 py = py + (double)(vy_ / (float)S.n);
             }
-            const double sm = px * ux + py * uy;
-            acc = acc + sm;
-            above += sm > thre2;
+            s_sm[q * 10 + t] = px * ux + py * uy;
         }
-        const double prior = 0.5 * (double)S.H / norm - 1.0;
-        const double sc = acc / 10.0 + (prior > 0.0 ? 0.0 : prior);
-        out[e] = (above > 8 && sc > 0.0) ? sc : -INFINITY;
+        __syncthreads();
+        if (live && t == 0) {
+            double acc = 0.0;
+            int above = 0;
+            for (int u = 0; u < 10; ++u) {
+                const double sm = s_sm[q * 10 + u];
+                acc = acc + sm;
+                above += sm > thre2;
+            }
+            const double prior = 0.5 * (double)S.H / norm - 1.0;
+            const double sc = acc / 10.0 + (prior > 0.0 ? 0.0 : prior);
+            out[e] = (above > 8 && sc > 0.0) ? sc : -INFINITY;
+        }
+        __syncthreads();
     }
 }
 
@@ -642,14 +670,33 @@ __global__ __launch_bounds__(256) void limb_greedy(const double* __restrict__ sc
     const double* sc = score + (size_t)nk * cap * cap;
     const int total = nA * nB, limit = nA < nB ? nA : nB;
     Conn* out = conn + (size_t)nk * cap;
+    // the first GR_REG * 256 pairs stay in registers (score, i, j) for all rounds; a used pair is
+    // retired to -inf in place (each round re-read every score from global memory before)
+    constexpr int GR_REG = 8;
+    double rv[GR_REG];
+    int ri[GR_REG], rj[GR_REG];
+#pragma unroll
+    for (int r = 0; r < GR_REG; ++r) {
+        const int e = tid + 256 * r;
+        ri[r] = e < total ? e / nB : 0;
+        rj[r] = e < total ? e - ri[r] * nB : 0;
+        rv[r] = e < total ? sc[e] : -INFINITY;
+    }
     for (;;) {
         double best = -INFINITY;
         int bidx = 0x7fffffff;
-        for (int e = tid; e < total; e += 256) {
+#pragma unroll
+        for (int r = 0; r < GR_REG; ++r) {  // e increases per thread, so ties keep the smaller index
+            if (rv[r] > best) {
+                best = rv[r];
+                bidx = tid + 256 * r;
+            }
+        }
+        for (int e = tid + 256 * GR_REG; e < total; e += 256) {
             const int i = e / nB, j = e - i * nB;
             if (s_used[i] | s_used[cap + j]) continue;
             const double v = sc[e];
-            if (v > best) {  // e increases per thread, so ties keep the smaller index
+            if (v > best) {
                 best = v;
                 bidx = e;
             }
@@ -677,6 +724,9 @@ __global__ __launch_bounds__(256) void limb_greedy(const double* __restrict__ sc
         if (bidx == 0x7fffffff || best == -INFINITY) break;
         const int i = bidx / nB, j = bidx - i * nB;
         const int c = s_count;
+#pragma unroll
+        for (int r = 0; r < GR_REG; ++r)
+            if (ri[r] == i || rj[r] == j) rv[r] = -INFINITY;
         if (tid == 0) {
             out[c].i = i;
             out[c].j = j;
@@ -850,15 +900,15 @@ void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre
 
 void launch_peaks_finalize(const int* cnt, const int* list, const double* list_score, int N, int H, int W,
                            const RecordLayout& L, uint8_t* records, int* peak_pos, int* part_cnt, hipStream_t st) {
-    hipLaunchKernelGGL(peaks_finalize, dim3(N), dim3(256), 0, st, cnt, list, list_score, H, W, L, records, peak_pos,
-                       part_cnt);
+    hipLaunchKernelGGL(peaks_finalize, dim3(N * 18), dim3(128), 0, st, cnt, list, list_score, H, W, L, records,
+                       peak_pos, part_cnt);
 }
 
 
 void launch_paf_score(const PafScales& S, const int* peak_pos, const int* part_cnt, int N, int cap, double thre2,
                       double* score, hipStream_t st) {
-    int by = (cap * cap + 255) / 256;
-    if (by > 16) by = 16;
+    int by = (cap * cap + PS_PAIRS - 1) / PS_PAIRS;
+    if (by > 64) by = 64;
     hipLaunchKernelGGL(paf_score, dim3(N * 19, by), dim3(256), 0, st, S, peak_pos, part_cnt, cap, thre2, score);
 }
 
