@@ -658,14 +658,12 @@ __global__ __launch_bounds__(256) void limb_greedy(const double* __restrict__ sc
     extern __shared__ unsigned char s_used[];  // [cap] A flags, [cap] B flags
     __shared__ double s_bs[4];
     __shared__ int s_bi[4];
-    __shared__ int s_count;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (nA == 0 || nB == 0) {
         if (tid == 0) conn_cnt[nk] = -1;  // special_k (src/body.py:153-155)
         return;
     }
     for (int i = tid; i < 2 * cap; i += 256) s_used[i] = 0;
-    if (tid == 0) s_count = 0;
     __syncthreads();
     const double* sc = score + (size_t)nk * cap * cap;
     const int total = nA * nB, limit = nA < nB ? nA : nB;
@@ -682,6 +680,7 @@ __global__ __launch_bounds__(256) void limb_greedy(const double* __restrict__ sc
         rj[r] = e < total ? e - ri[r] * nB : 0;
         rv[r] = e < total ? sc[e] : -INFINITY;
     }
+    int count = 0;
     for (;;) {
         double best = -INFINITY;
         int bidx = 0x7fffffff;
@@ -723,23 +722,22 @@ __global__ __launch_bounds__(256) void limb_greedy(const double* __restrict__ sc
             }
         if (bidx == 0x7fffffff || best == -INFINITY) break;
         const int i = bidx / nB, j = bidx - i * nB;
-        const int c = s_count;
 #pragma unroll
         for (int r = 0; r < GR_REG; ++r)
             if (ri[r] == i || rj[r] == j) rv[r] = -INFINITY;
         if (tid == 0) {
-            out[c].i = i;
-            out[c].j = j;
-            out[c].s = best;
+            out[count].i = i;
+            out[count].j = j;
+            out[count].s = best;
             s_used[i] = 1;
             s_used[cap + j] = 1;
-            s_count = c + 1;
         }
         __syncthreads();
-        if (c + 1 >= limit) break;
+        // the count lives in every thread's registers: a shared counter bumped by thread 0 could
+        // be read after the bump by a slower wave, which then left the loop a round early
+        if (++count >= limit) break;
     }
-    __syncthreads();
-    if (tid == 0) conn_cnt[nk] = s_count;
+    if (tid == 0) conn_cnt[nk] = count;
 }
 
 // One wavefront per frame: sequential person assembly with lane-parallel row scans.
