@@ -8,7 +8,9 @@ from src.body import Body
 from src.weights import BENCH_OUT_SCALE, seeded_state_dict
 body = Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE))
 rng = np.random.default_rng(21)
-batches = [rng.integers(0, 256, (3, 184, 328, 3), dtype=np.uint8) for _ in range(3)]
+# BENCH=1: the bench's shape (32 frames of 368x656 per call) instead of 3 frames of 184x328
+NB, HB, WB = (32, 368, 656) if os.environ.get("BENCH") == "1" else (3, 184, 328)
+batches = [rng.integers(0, 256, (NB, HB, WB, 3), dtype=np.uint8) for _ in range(3)]
 exp = [body.batch(f) for f in batches]
 dev = [torch.from_numpy(f).cuda() for f in batches]
 torch.cuda.synchronize()
@@ -30,5 +32,6 @@ for trial in range(T):
                     d = [r for r in range(rows) if not np.array_equal(s[r], es[r])]
                     print(f"  trial {trial} call {call} b{i} f{f}: subset {s.shape} vs {es.shape}, first diff row "
                           f"{d[:1]}: {s[d[0]] if d else None} vs {es[d[0]] if d else None}", flush=True)
-print(f"lib={os.environ.get('OPOSE_LIB', 'head')} small_ovh={os.environ.get('OPOSE_X6_SMALL_OVH', '1')}: "
+print(f"lib={os.environ.get('OPOSE_LIB', 'head')} small_ovh={os.environ.get('OPOSE_X6_SMALL_OVH', '1')} "
+      f"shape={NB}x{HB}x{WB}: "
       f"{frames} frames, candidate mismatches {bad_c}, subset-only mismatches {bad_s}", flush=True)
