@@ -1571,7 +1571,10 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
             upsample_to_mid(h, s, S, 185, N, g, 56);
         };
         auto net_part = [&] {
-            for (int s = 0; s < p.n_scales; ++s) scale_net(s);
+            if (h->scale_streams && p.n_scales > 1)  // (pipelined: forked from and joined into nstream)
+                run_scales_concurrently(h, p.n_scales, scale_net);
+            else
+                for (int s = 0; s < p.n_scales; ++s) scale_net(s);
         };
         if (h->pipeline && (flags & OPOSE_PIPELINE) && (flags & OPOSE_IN_DEVICE) && (flags & OPOSE_OUT_DEVICE)) {
             pipelined_body(h, N, H, W, gs, p, rec, net_part);

@@ -6,7 +6,9 @@ import torch
 sys.path.insert(0, "pytorch-openpose_amd")
 from src.body import Body
 from src.weights import BENCH_OUT_SCALE, seeded_state_dict
-body = Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE))
+# MULTI=1: a two-scale pyramid (scale_search 0.5, 1.0: the scales' networks run concurrently)
+scales = (0.5, 1.0) if os.environ.get("MULTI") == "1" else (0.5,)
+body = Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE), scale_search=scales)
 rng = np.random.default_rng(21)
 # BENCH=1: the bench's shape (32 frames of 368x656 per call) instead of 3 frames of 184x328
 NB, HB, WB = (32, 368, 656) if os.environ.get("BENCH") == "1" else (3, 184, 328)
@@ -33,5 +35,5 @@ for trial in range(T):
                     print(f"  trial {trial} call {call} b{i} f{f}: subset {s.shape} vs {es.shape}, first diff row "
                           f"{d[:1]}: {s[d[0]] if d else None} vs {es[d[0]] if d else None}", flush=True)
 print(f"lib={os.environ.get('OPOSE_LIB', 'head')} small_ovh={os.environ.get('OPOSE_X6_SMALL_OVH', '1')} "
-      f"shape={NB}x{HB}x{WB}: "
+      f"shape={NB}x{HB}x{WB} scales={len(scales)}: "
       f"{frames} frames, candidate mismatches {bad_c}, subset-only mismatches {bad_s}", flush=True)
