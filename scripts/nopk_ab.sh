@@ -1,5 +1,7 @@
 # Packed-FP32 A/B: screened-NMS self-checks under overlap and the bench line, for the shipped
-# library (no packed FP32) and alt_lib/pk.so (compiler default).
+# library (no packed FP32) and alt_lib/pk.so (compiler default).  Historical record of the round-2
+# root-cause run: the screened NMS and its debug script have since been deleted, so
+# this no longer runs as is; scripts/pipeline_stress.sh is the current pipelined-records check.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONDONTWRITEBYTECODE=1
 bash scripts/gauss_debug.sh main || true
 for tag in main pk main pk; do
