@@ -249,7 +249,7 @@ def host_to_host(body, frames_np, steps, dev, rank, world):
     rdev = [torch.empty((B, rb), dtype=torch.uint8, device=dev) for _ in range(2)]
     rhost = [torch.empty((B, rb), dtype=torch.uint8).pin_memory() for _ in range(2)]
     cps = [torch.cuda.Stream(device=dev) for _ in range(2)]
-    lib_stream = torch.cuda.ExternalStream(body.handle.stream(), device=dev)
+    lib_stream = body.handle.torch_stream()
     from src.dist import gather_records
 
     def upload(i):
@@ -361,7 +361,7 @@ def main():
     frames = torch.from_numpy(frames_np).to(dev)
     rb = body.handle.record_bytes()
     rec = torch.empty((B, rb), dtype=torch.uint8, device=dev)
-    lib_stream = torch.cuda.ExternalStream(body.handle.stream(), device=dev)
+    lib_stream = body.handle.torch_stream()
     torch.cuda.synchronize()
     from src.dist import gather_records
 

@@ -45,27 +45,37 @@ struct ConvArgs {
     int tap_major;      // K ordered (tap, channel) with Cin padded to 32 (else OIHW + ktab)
     int ngroups;        // 1 or 2 GEMM groups sharing the launch
     int sk_grid;        // stream-K workgroups (== tiles: plain data-parallel grid)
-    float* partial;     // stream-K partial slabs [2 * sk_grid][MT * PT]
-    int* sk_cnt;        // per-tile arrival counters (zero between launches) -> the last
-                        // workgroup of a split tile reduces it; nullptr: conv_sk_fixup launch
+    float* partial;     // stream-K partial slabs [2 * sk_grid][MT * PT] (summed by conv_sk_fixup)
 };
 
 // ---------------------------------------------------------------- split-bf16 ("x6") convolution
 // Activation format X6: every fp32 value x is stored as three bfloat16 pieces x0 + x1 + x2 == x
 // (exact: round-to-nearest bf16 of x, of the remainder, of the remainder's remainder -> 24
-// significant bits = the whole fp32 significand).  Layout per piece plane: [N][Cg][H*W][8]
-// (8 channels of a pixel contiguous = one 16-byte unit); the three planes follow each other
-// at `ps` bytes.  Channel offsets / strides are in groups of 8 channels.
+// significant bits = the whole fp32 significand).  8 channels of a pixel form one 16-byte unit;
+// the three piece planes follow each other at `ps` bytes.  Within a plane a unit is addressed by
+// an X6Layout: unit(n, g, y, x) = o0 + n * fs + g * gs + y * rs + x (g = group relative to the
+// slice, o0 includes the slice's first group).  Two layouts are used:
+//  * dense  [N][Cg][H*W]:  fs = Cg*H*W, gs = H*W, rs = W, o0 = goff*H*W (trunk activations);
+//  * padded (X6P, the low-resolution CPM stage buffers): per group one tall image of the N
+//    frames stacked with 3 zero rows above, between and below them and 3 zero units between
+//    consecutive rows (row pitch P = W + 3, pixel (n, y, x) at row 3 + n*(H+3) + y, column
+//    3 + x), plus one zero row at the end: every tap of a 7x7 / 3x3 / 1x1 'same' conv is a
+//    constant shift dy*P + dx of the pixel's unit, and the window of a run of consecutive
+//    pixels is contiguous across rows and frames (conv7_win_x6).  fs = (H+3)*P, gs =
+//    (N*(H+3)+4)*P, rs = P, o0 = goff*gs + 3*P + 3.  The zero units are never written.
+struct X6Layout {
+    uint32_t fs, gs, rs, o0;
+};
+
 struct X6Group {
-    const uint8_t* in;     // X6 buffer (plane 0, frame 0, group 0)
+    const uint8_t* in;     // X6 buffer (plane 0)
     const uint8_t* wt;     // [nK][3 pieces][4 groups][Mpad] units of 8 bf16
     const float* bias;     // [cout]
     void* out;             // X6 buffer, or fp32 NCHW when out_f32
-    void* out2;            // optional duplicate destination, same format (nullptr = none)
+    void* out2;            // optional duplicate destination, X6 (nullptr = none)
     uint32_t in_ps, out_ps, out2_ps;  // piece strides (bytes) of the X6 buffers
-    int in_cg, in_goff;    // groups per frame of the input buffer / first group read
-    int out_c, out_off;    // X6: groups per frame / first group; fp32: channels / first channel
-    int out2_c, out2_off;
+    X6Layout in_l, out_l, out2_l;     // unit addressing of the X6 slices
+    int out_c, out_off;    // fp32 output: channels per frame / first channel
     int cout, relu, out_f32;
 };
 
@@ -77,7 +87,6 @@ struct X6Args {
     int nK;         // chunks of 32 k
     int Mpad, npix, ngroups, sk_grid;
     float* partial; // stream-K partial slabs [2 * sk_grid][MT * PT]
-    int ablate;     // timing ablations (0 in production): 1 no im2col DMA, 2 no weight DMA, 4 no barrier, 8 no LDS reads
     int pool;       // 1: 2x2/2 max-pool fused into the epilogue (npix = N * (H/2) * (W/2) * 4, quad-major)
 };
 

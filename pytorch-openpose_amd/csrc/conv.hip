@@ -45,58 +45,7 @@ constexpr int wg_waves(int mt, int pt) { return mt * pt >= 32768 ? 8 : 4; }
 // channels -- 4 MB of live gathers per XCD, which thrashed L2).  Layers with Cin >= 32; else K is
 // the OIHW flattening decoded through `ktab` (conv1_1: K = 27).
 // KS: compile-time kernel size (1, 3, 7) so the tap decode folds; 0 = runtime a.ks.
-// ABL: timing-only ablations (never launched in production): 1 skip the im2col gather,
-// 2 skip the weight load, 4 skip the LDS fragment reads, 8 skip the per-chunk barrier,
-// 16 gather from cache-hot addresses (same rows every chunk), 32 cache-hot weight rows,
-// 128 barrier without waiting for the stage's DMA (wrong results; latency probe).
-// device-coherent 16-byte load (sc1: served from the coherence point, not a possibly stale
-// line in this XCD's L2) -- reads partial slabs written by other workgroups in this launch
-__device__ __forceinline__ f32x4 load_sc1(const float* p) {
-    f32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-
-// Sum the partial slabs of `tile` (workgroups w0..w1, k order) + bias + ReLU -> channel slice.
-// Called by the last workgroup to finish a part of the tile; mirrors conv_sk_fixup.
-template <int MT, int PT, int NTH>
-__device__ __forceinline__ void reduce_tile(const ConvArgs& a, const ConvGroup& G, int tile, int m0, int p0, int w0,
-                                            int w1, int nK, long long I, int Gw, const float* s_bias, int HW) {
-    for (int e = threadIdx.x * 4; e < MT * PT; e += NTH * 4) {
-        const int ml = e / PT, pl = e - ml * PT;
-        const int m = m0 + ml;
-        if (m >= G.cout) continue;
-        f32x4 v;
-        for (int w = w0; w <= w1; w += 4) {  // 4 loads in flight, summed in k order
-            f32x4 part[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int ww = min(w + u, w1);
-                const long long lo_w = (long long)ww * I / Gw;
-                const int slot = (lo_w / nK == tile) ? 2 * ww : 2 * ww + 1;
-                part[u] = load_sc1(a.partial + (size_t)slot * (MT * PT) + e);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(part[0]), "+v"(part[1]), "+v"(part[2]), "+v"(part[3]));
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (w + u <= w1) v = (w + u == w0) ? part[u] : v + part[u];
-        }
-        const float bias = s_bias[ml];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int p = p0 + pl + k;
-            if (p >= a.npix) break;
-            float o = v[k] + bias;
-            if (G.relu) o = fmaxf(o, 0.f);
-            const int n = p / HW;
-            const int rem = p - n * HW;
-            G.out[((size_t)n * G.out_cstride + G.out_coff + m) * HW + rem] = o;
-            if (G.out2) G.out2[((size_t)n * G.out2_cstride + G.out2_coff + m) * HW + rem] = o;
-        }
-    }
-}
-
-template <int MT, int PT, bool TAP, int KS, int ABL = 0>
+template <int MT, int PT, bool TAP, int KS>
 __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void conv_igemm_f32(
     ConvArgs a, const int* __restrict__ ktab) {
     const int ks = KS ? KS : a.ks;
@@ -111,7 +60,6 @@ __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void c
     // [2 stages][A tile KC x MT | B tile KC x PT] + bias; both tiles are filled by LDS-DMA
     // (buffer/global_load ... lds): no register staging, no ds_write pass.
     __shared__ __attribute__((aligned(16))) float lds[2 * (A_SZ + B_SZ) + MT];
-    __shared__ int s_last;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -212,7 +160,6 @@ __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void c
         };
         // issue the LDS-DMA of B row r (this wave's) of chunk c into stage `buf`
         auto dma_b_row = [&](int c, int buf, int r) __attribute__((always_inline)) {
-            if constexpr ((ABL & 1) != 0) return;
             float* Bs = lds + buf * (A_SZ + B_SZ) + A_SZ + (wave * RW + r) * PT;
             if constexpr (TAP) {
                 const int ch = min(ch0 + r, a.Cin - 1);  // padded channels: any valid address (weights are 0)
@@ -221,7 +168,7 @@ __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void c
                 for (int j = 0; j < PJ; ++j)
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(
                         rsrc, (lds_ptr_t)(Bs + j * 64), 4,
-                        (ABL & 16) ? poff[j] * 4u + (uint32_t)r * HW4 : base[j] + choff, 0, 0, 0);
+                        base[j] + choff, 0, 0, 0);
             } else {
                 const int code = ktab[c * KC + wave * RW + r];  // (c << 8) | (ky << 4) | kx
                 const int cch = code >> 8;
@@ -238,8 +185,7 @@ __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void c
             }
         };
         auto dma_a = [&](int c, int buf) __attribute__((always_inline)) {
-            if constexpr ((ABL & 2) != 0) return;
-            const int k0 = (ABL & 32) ? 0 : c * KC;
+            const int k0 = c * KC;
             float* As = lds + buf * (A_SZ + B_SZ);
 #pragma unroll
             for (int i = 0; i < A_PW; ++i) {
@@ -274,21 +220,15 @@ __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void c
             float av[2][TM], bv[2][TN];
             auto read_frags = [&](int step, float (&fa)[TM], float (&fb)[TN]) __attribute__((always_inline)) {
 #pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    if constexpr ((ABL & 4) != 0) fa[i] = (float)(lane + i + step);
-                    else
-                        asm volatile("ds_read_b32 %0, %1 offset:%2"
-                                     : "=v"(fa[i])
-                                     : "v"(a_lds), "i"((2 * step * MT + i * 32) * 4));
-                }
+                for (int i = 0; i < TM; ++i)
+                    asm volatile("ds_read_b32 %0, %1 offset:%2"
+                                 : "=v"(fa[i])
+                                 : "v"(a_lds), "i"((2 * step * MT + i * 32) * 4));
 #pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    if constexpr ((ABL & 4) != 0) fb[j] = (float)(lane - j - step);
-                    else
-                        asm volatile("ds_read_b32 %0, %1 offset:%2"
-                                     : "=v"(fb[j])
-                                     : "v"(b_lds), "i"((2 * step * PT + j * 32) * 4));
-                }
+                for (int j = 0; j < TN; ++j)
+                    asm volatile("ds_read_b32 %0, %1 offset:%2"
+                                 : "=v"(fb[j])
+                                 : "v"(b_lds), "i"((2 * step * PT + j * 32) * 4));
             };
             read_frags(0, av[0], bv[0]);
 #pragma unroll
@@ -298,23 +238,19 @@ __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void c
                 if (ks2 < RW) dma_b_row(cn, buf ^ 1, ks2);
                 // wait for this step's fragments only (the next step's stay in flight); the "+v"
                 // operands order the MFMAs after the wait
-                if constexpr ((ABL & 4) == 0) {
-                    if (ks2 + 1 < KC / 2) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TM + TN));
-                    else asm volatile("s_waitcnt lgkmcnt(0)");
+                if (ks2 + 1 < KC / 2) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TM + TN));
+                else asm volatile("s_waitcnt lgkmcnt(0)");
 #pragma unroll
-                    for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(av[cur][i]));
+                for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(av[cur][i]));
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bv[cur][j]));
-                }
+                for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bv[cur][j]));
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
             }
-            if constexpr ((ABL & 128) != 0) asm volatile("s_barrier" ::: "memory");  // no DMA wait (timing only)
-            else if constexpr ((ABL & 8) == 0) __syncthreads();  // next stage landed everywhere; this stage free
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // next stage landed everywhere; this stage free
         }
 
         // ---- epilogue: whole tile -> bias + ReLU into the channel slice; part of a tile ->
@@ -357,259 +293,7 @@ __global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void c
                     }
                 }
         }
-        // ---- stream-K reduction: the last workgroup to finish a part of this tile sums all the
-        // parts in k order (deterministic, same order as conv_sk_fixup) + bias + ReLU.
-        if (!whole && a.sk_cnt) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab stores are acked
-            __syncthreads();
-            const long long x0 = (long long)tile * nK;
-            const int w0 = (int)(((x0 + 1) * Gw - 1) / I);   // workgroups holding the tile's
-            const int w1 = (int)(((x0 + nK) * Gw - 1) / I);  // first / last chunk
-            if (tid == 0) s_last = atomicAdd(a.sk_cnt + tile, 1) == w1 - w0;
-            __syncthreads();
-            if (s_last) {
-                reduce_tile<MT, PT, 64 * NW>(a, G, tile, m0, p0, w0, w1, nK, I, Gw, s_bias, HW);
-                if (tid == 0) atomicExch(a.sk_cnt + tile, 0);  // ready for the next launch
-            }
-        }
     }
-}
-
-// ---------------------------------------------------------------------------------------
-// Window variant for 3x3 / 7x7 layers whose rows are short (W <= ~80): instead of gathering
-// the im2col rows of every (tap, channel) chunk (KS*KS DMA passes over the same activations),
-// the workgroup stages, once per 32-channel block, the contiguous flat window
-//   win[c][q] = in[c][p0 - PAD*W - PAD + q],   q < PT + 2*PAD*W + 2*PAD
-// (flat over (frame, y, x)) and reads the B fragment of tap (dy, dx) for pixel p at
-//   q = (p - p0) + dy*W + dx + PAD*W + PAD.
-// A valid tap of p always lands inside p's own frame (0 <= y+dy < H, 0 <= x+dx < W), so one
-// flat window serves every tap across row and frame boundaries; invalid taps (zero padding)
-// are masked to 0 after the LDS read.  The window DMA is 25x (7x7) / 5x (3x3) fewer
-// instructions than the im2col gather and is double-buffered across channel blocks;
-// weights (A) still stream per 32-k chunk through two LDS stages.  K order, stream-K
-// ranges, partial slabs and the fixup are those of conv_igemm_f32.
-template <int MT, int PT, int KS>
-__global__ __launch_bounds__(64 * wg_waves(MT, PT), 8 / wg_waves(MT, PT)) void conv_window_f32(ConvArgs a) {
-    constexpr int PAD = KS / 2, TAPS = KS * KS;
-    constexpr int NW = wg_waves(MT, PT), NWM = NW == 8 ? MT / 64 : 2, NWP = NW / NWM;
-    constexpr int WM = MT / NWM, WP = PT / NWP;
-    constexpr int TM = WM / 32, TN = WP / 32;
-    constexpr int A_SZ = KC * MT;
-    constexpr int A_PW = A_SZ / 256 / NW;   // 1-KiB A pieces per wave per chunk
-    constexpr int CPW = KC / NW;            // window channels loaded per wave
-
-    extern __shared__ __attribute__((aligned(16))) float lds[];  // [2][A] [2][KC][WS]
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int l31 = lane & 31, hk = lane >> 5;
-    const int W = a.W, H = a.H, HW = H * W;
-    const uint32_t HW4 = (uint32_t)HW * 4u;
-    const int halo = PAD * W + PAD;
-    const int WLEN = PT + 2 * halo;
-    const int WS = (WLEN + 3) & ~3;   // channel stride of a window (floats)
-    const int NQ = (WLEN + 63) / 64;  // 64-float DMA pieces per channel
-    float* const wins = lds + 2 * A_SZ;
-    const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
-    const int nK = a.Kpad / KC;
-    const int wm0 = (wave % NWM) * WM;
-    const int wp0 = (wave / NWM) * WP;
-
-    const int Gw = gridDim.x;
-    const int b = blockIdx.x;
-    const int q8 = Gw >> 3, rr = Gw & 7, xcd = b & 7;
-    const int id = xcd * q8 + min(xcd, rr) + (b >> 3);
-    const long long I = (long long)nM * nP * a.ngroups * nK;
-    const long long lo = (long long)id * I / Gw, hi = (long long)(id + 1) * I / Gw;
-
-    // Segments run last-first: a range is [tail of tile t | whole tiles | head of tile t'], and
-    // processing the head (k = 0 ..) before the tail (k = c0 ..) keeps every workgroup of an XCD
-    // at nearly the same k chunk at the same time -- they then share each weight tile in L2
-    // (forward order spreads the live k positions over the whole weight matrix: 3-6 MB, more
-    // than an XCD's L2).  The partial slot stays tied to the range start (see conv_sk_fixup).
-    for (long long itp = hi; itp > lo;) {
-        const int tile = (int)((itp - 1) / nK);
-        const int c_end = (int)(itp - (long long)tile * nK);
-        const int c_begin = (int)max<long long>(0, lo - (long long)tile * nK);
-        itp = (long long)tile * nK + c_begin;
-        const int first = itp == lo;  // the segment holding the range start -> slot 2*id
-        const int mt = tile % nM;
-        const int rest = tile / nM;
-        const int pt = rest % nP;
-        const int g = rest / nP;
-        const ConvGroup G = g == 0 ? a.g[0] : a.g[1];
-        const int p0 = pt * PT;
-        const int m0 = mt * MT;
-
-        __syncthreads();  // the previous segment is done with every LDS buffer
-
-        const float* in_base = G.in + (size_t)G.in_coff * HW;
-        const __amdgpu_buffer_rsrc_t rsrc =
-            __builtin_amdgcn_make_buffer_rsrc((void*)in_base, (short)0, (int)0x80000000u, 0x00020000);
-
-        // window DMA sources of this lane: byte offset (channel 0) of window position
-        // i * 64 + lane for every piece i (<= 16); invalid -> >= 3 GiB (range check -> 0.0f)
-        uint32_t wsrc[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int t = p0 - halo + i * 64 + lane;  // virtual flat index
-            const int f = t >= 0 ? t / HW : -1;
-            const bool ok = t >= 0 && f < a.N;
-            wsrc[i] = ok ? (uint32_t)(f * G.in_cstride * HW + (t - f * HW)) * 4u : 0xC0000000u;
-        }
-        // the lane's fragment pixels (B column l31 of each 32-pixel block j)
-        int py[TN], px[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int p = p0 + wp0 + j * 32 + l31;
-            const bool v = p < a.npix;
-            const int r = (v ? p : 0) % HW;
-            py[j] = v ? r / W : -100000;
-            px[j] = r - (r / W) * W;
-        }
-
-        // issue this wave's share (CPW channels x NQ pieces) of channel block cb's window
-        auto dma_window = [&](int cb, int wb) __attribute__((always_inline)) {
-            float* wdst = wins + wb * (KC * WS) + wave * CPW * WS;
-            const int ch0 = cb * KC + wave * CPW;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                if (i < NQ) {  // wave-uniform
-#pragma unroll
-                    for (int cw = 0; cw < CPW; ++cw) {
-                        // padded channels: any finite data (their weights are 0)
-                        const uint32_t choff = (uint32_t)min(ch0 + cw, a.Cin - 1) * HW4;
-                        if (i * 64 + lane < WLEN)
-                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wdst + cw * WS + i * 64), 4,
-                                                                    wsrc[i] + choff, 0, 0, 0);
-                    }
-                }
-            }
-        };
-        auto dma_a = [&](int c, int buf) __attribute__((always_inline)) {
-            const int k0 = c * KC;
-            float* As = lds + buf * A_SZ;
-#pragma unroll
-            for (int i = 0; i < A_PW; ++i) {
-                const int piece = wave * A_PW + i;
-                const int f = piece * 256 + lane * 4;
-                const int row = f / MT, col = f - row * MT;
-                __builtin_amdgcn_global_load_lds((const void*)(G.wt + (size_t)(k0 + row) * a.Mpad + m0 + col),
-                                                 (lds_ptr_t)(As + piece * 256), 16, 0, 0);
-            }
-        };
-
-        floatx16 acc[TM][TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-        const int blk0 = c_begin / TAPS, blk_last = (c_end - 1) / TAPS;
-        dma_window(blk0, 0);
-        dma_a(c_begin, 0);
-        __syncthreads();  // first window and A stage landed
-        for (int c = c_begin; c < c_end; ++c) {
-            const int buf = (c - c_begin) & 1;
-            const int blk = c / TAPS, tap = c - blk * TAPS;
-            const int wb = (blk - blk0) & 1;
-            const int cn = min(c + 1, c_end - 1);
-            dma_a(cn, buf ^ 1);
-            // the next block's window streams in during this block (issued at its first chunk)
-            if ((tap == 0 || c == c_begin) && blk < blk_last) dma_window(blk + 1, wb ^ 1);
-            const int ky = tap / KS;
-            const int dy = ky - PAD, dx = tap - ky * KS - PAD;
-            const uint32_t a_lds = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * A_SZ + wm0 + l31 + hk * MT);
-            const uint32_t b_lds = (uint32_t)(uintptr_t)(lds_ptr_t)(wins + wb * (KC * WS) + hk * WS + wp0 + l31 +
-                                                                    dy * W + dx + halo);
-            bool ok[TN];
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                ok[j] = (unsigned)(py[j] + dy) < (unsigned)H && (unsigned)(px[j] + dx) < (unsigned)W;
-            float av[2][TM], bv[2][TN];
-            auto read_frags = [&](int step, float (&fa)[TM], float (&fb)[TN]) __attribute__((always_inline)) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-                    asm volatile("ds_read_b32 %0, %1 offset:%2"
-                                 : "=v"(fa[i])
-                                 : "v"(a_lds), "i"((2 * step * MT + i * 32) * 4));
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(fb[j]) : "v"(b_lds + 2u * step * WS * 4u),
-                                 "i"(j * 32 * 4));
-            };
-            read_frags(0, av[0], bv[0]);
-#pragma unroll
-            for (int ks2 = 0; ks2 < KC / 2; ++ks2) {
-                const int cur = ks2 & 1, nxt = cur ^ 1;
-                if (ks2 + 1 < KC / 2) read_frags(ks2 + 1, av[nxt], bv[nxt]);
-                if (ks2 + 1 < KC / 2) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TM + TN));
-                else asm volatile("s_waitcnt lgkmcnt(0)");
-#pragma unroll
-                for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(av[cur][i]));
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    asm volatile("" : "+v"(bv[cur][j]));
-                    bv[cur][j] = ok[j] ? bv[cur][j] : 0.f;  // zero padding / other rows and frames
-                }
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
-            }
-            __syncthreads();  // next A stage (and, at a block end, the next window) landed; this stage free
-        }
-
-        const bool whole = c_begin == 0 && c_end == nK;
-        float* slab = a.partial + (size_t)(2 * id + (first ? 0 : 1)) * (MT * PT);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int pl = wp0 + j * 32 + l31;
-            const int p = p0 + pl;
-            if (!whole) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int ml = wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-                        asm volatile("global_store_dword %0, %1, off sc1" ::"v"(slab + ml * PT + pl),
-                                     "v"(acc[i][j][r])
-                                     : "memory");
-                    }
-                continue;
-            }
-            if (p >= a.npix) continue;
-            const int n = p / HW;
-            const int rem = p - n * HW;
-            float* ob = G.out + ((size_t)n * G.out_cstride + G.out_coff) * HW + rem;
-            float* ob2 = G.out2 ? G.out2 + ((size_t)n * G.out2_cstride + G.out2_coff) * HW + rem : nullptr;
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-                    if (m < G.cout) {
-                        float v = acc[i][j][r] + G.bias[m];
-                        if (G.relu) v = fmaxf(v, 0.f);
-                        ob[(size_t)m * HW] = v;
-                        if (ob2) ob2[(size_t)m * HW] = v;
-                    }
-                }
-        }
-    }
-}
-
-// LDS bytes of conv_window_f32 for a layer (0: the window does not fit -> im2col kernel)
-size_t conv_window_lds_bytes(int mt, int pt, int ks, int W) {
-    const int halo = (ks / 2) * W + ks / 2;
-    const int wlen = pt + 2 * halo;
-    if (wlen > 16 * 64) return 0;
-    const size_t bytes = (size_t)(2 * KC * mt + 2 * KC * ((wlen + 3) & ~3)) * 4;
-    return bytes <= 160 * 1024 ? bytes : 0;
 }
 
 // Stream-K fixup: grid (tiles, MT*PT/1024); each thread finishes 4 consecutive pixels of one
@@ -704,48 +388,8 @@ static void launch_tile(const ConvArgs& a, const int* ktab, hipStream_t st) {
     else
         hipLaunchKernelGGL((conv_igemm_f32<MT, PT, true, 0>), grid, dim3(NTH), 0, st, a, ktab);
     const int tiles = (a.Mpad / MT) * ((a.npix + PT - 1) / PT) * a.ngroups;
-    if (a.sk_grid != tiles && !a.sk_cnt)
-        hipLaunchKernelGGL((conv_sk_fixup<MT, PT>), dim3(tiles, MT * PT / 1024), dim3(256), 0, st, a);
-}
-
-template <int MT, int PT, int KS>
-static void launch_window_ks(const ConvArgs& a, size_t lds_bytes, hipStream_t st) {
-    static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_window_f32<MT, PT, KS>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        return true;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL((conv_window_f32<MT, PT, KS>), dim3(a.sk_grid), dim3(64 * wg_waves(MT, PT)), lds_bytes, st, a);
-    const int tiles = (a.Mpad / MT) * ((a.npix + PT - 1) / PT) * a.ngroups;
     if (a.sk_grid != tiles)
         hipLaunchKernelGGL((conv_sk_fixup<MT, PT>), dim3(tiles, MT * PT / 1024), dim3(256), 0, st, a);
-}
-
-bool launch_conv_window(const ConvArgs& a, int mt, int pt, hipStream_t st) {
-    if (!a.tap_major || (a.ks != 3 && a.ks != 7) || mt != 128 || pt != 256) return false;
-    if ((double)a.Cin * a.H * a.W * 4.0 >= 1073741824.0) return false;  // invalid-offset headroom
-    const size_t bytes = conv_window_lds_bytes(mt, pt, a.ks, a.W);
-    if (!bytes) return false;
-    if (a.ks == 7) launch_window_ks<128, 256, 7>(a, bytes, st);
-    else launch_window_ks<128, 256, 3>(a, bytes, st);
-    return true;
-}
-
-void launch_conv_ablation(const ConvArgs& a, int ablate, hipStream_t st) {
-    const dim3 grid(a.sk_grid);
-    switch (ablate) {
-        case 3: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 3>), grid, dim3(256), 0, st, a, nullptr); break;
-        case 7: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 7>), grid, dim3(256), 0, st, a, nullptr); break;
-        case 11: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 11>), grid, dim3(256), 0, st, a, nullptr); break;
-        case 15: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 15>), grid, dim3(256), 0, st, a, nullptr); break;
-        case 1: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 1>), grid, dim3(256), 0, st, a, nullptr); break;
-        case 16: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 16>), grid, dim3(256), 0, st, a, nullptr); break;
-        case 32: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 32>), grid, dim3(256), 0, st, a, nullptr); break;
-        case 48: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 48>), grid, dim3(256), 0, st, a, nullptr); break;
-        case 128: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 128>), grid, dim3(256), 0, st, a, nullptr); break;
-        default: hipLaunchKernelGGL((conv_igemm_f32<128, 128, true, 7, 2>), grid, dim3(256), 0, st, a, nullptr); break;
-    }
 }
 
 void launch_conv(const ConvArgs& a, const int* ktab, int mt, int pt, hipStream_t st) {

@@ -1,0 +1,390 @@
+// conv_win.hip — the 7x7 CPM convolutions (src/model.py:71-85 Mconv1-5 of stages 2-6, body and
+// hand) as split-bf16 implicit GEMMs whose im2col operand comes from an input window in LDS.
+//
+// conv_x6 streams the im2col tile of every 32-deep k chunk through L2 into LDS by LDS-DMA: at
+// 7x7 each input unit travels 49 times, 2/3 of the kernel's DMA instructions and LDS-DMA bytes.
+// Here the input is the padded X6P layout (common.h): every tap of a pixel is the unit at a
+// constant shift dy*P + dx, and the units of a run of PT consecutive pixels (across rows and
+// frames) plus its 3-row halo form one contiguous range of each (piece, group) plane.  So a
+// workgroup DMAs, per input channel group, that window (3 pieces x L <= WMAX units, once per 49
+// taps) and reads the B fragment of (group, tap) for pixel p at window position wpos(p) + dy*P +
+// dx with ds_read_b128.
+//  * K order (pair order): k = (pair q, channel c of its group), pair q = (group q / 49, tap
+//    q % 49), chunk = 4 consecutive pairs = the four 8-k groups of a 16x16x32 MFMA k-step; the
+//    weights are packed in this order (x6_pack_weights_pairs).  A chunk may span two channel
+//    groups: two window buffers, group g in buffer g & 1, the window of group g + 2 DMA'd right
+//    after the barrier of the last chunk that reads group g (>= 10 chunks before its first use).
+//  * Everything else is conv_x6's MODE-2 loop: 128 x 256 tile, 8 waves of 64 x 64, weights by
+//    LDS-DMA into two stages, six piece products per chunk in the order
+//    (0,2) (0,0) (0,1) | barrier | (1,0) (2,0) (1,1), fragments refilled after their last use.
+//  * Whole tiles only (data-parallel grid of >= ~200 tiles: the batched path); the host falls
+//    back to conv_x6 (stream-K) for small problems and when a window would exceed WMAX.
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+#include "x6.h"
+
+namespace opose {
+
+template <int MT, int PT, int KS, int WMAX>
+__global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a) {
+    constexpr int TAPS = KS * KS, PAD = KS / 2;
+    constexpr int NW = x6_waves(MT, PT), NWM = NW == 8 ? MT / 64 : 2, NWP = NW / NWM;
+    constexpr int WM = MT / NWM, WP = PT / NWP;
+    constexpr int TM = WM / 16, TN = WP / 16;
+    constexpr int A_U = 12 * MT;                 // 16-byte units per weight stage
+    constexpr int A_PW = A_U / 64 / NW;          // weight DMA instructions per wave per chunk
+    constexpr int WBUF = 3 * WMAX;               // units per window buffer (3 pieces)
+    static_assert(A_U % (64 * NW) == 0 && A_PW == 3 && WMAX % 64 == 0 && TAPS >= 16, "conv_win_x6 tile");
+
+    __shared__ __attribute__((aligned(16))) uint4 lds[2 * A_U + 2 * WBUF];
+    __shared__ float s_bias[MT];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
+    const int nK = a.nK;
+    const int H = a.H, W = a.W, HW = H * W;
+    const int wm0 = (wave % NWM) * WM;
+    const int wp0 = (wave / NWM) * WP;
+
+    int tile;
+    {
+        const int Gw = gridDim.x, b = blockIdx.x;
+        const int q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
+        tile = xcd * q + min(xcd, rr) + (b >> 3);  // XCD-contiguous tiles (guide T1)
+    }
+    const int mt = tile % nM;
+    const int rest = tile / nM;
+    const int ptl = rest % nP;
+    const int gsel = rest / nP;
+    const X6Group G = gsel == 0 ? a.g[0] : a.g[1];
+    const int p0 = ptl * PT, m0 = mt * MT;
+    if (tid < MT) s_bias[tid] = (m0 + tid < G.cout) ? G.bias[m0 + tid] : 0.f;
+
+    // ---- window geometry (wave-uniform): padded rows R of the tile's first / last pixel
+    const int P = (int)G.in_l.rs;
+    auto prow = [&](int p) __attribute__((always_inline)) {
+        const int n = p / HW, y = (p - n * HW) / W;
+        return 3 + n * (H + 3) + y;
+    };
+    const int p_last = min(p0 + PT, a.npix) - 1;
+    const int R0 = prow(p0), R1 = prow(p_last);
+    const int ws = (R0 - PAD) * P;                                // window start (unit of the plane)
+    const int L = (R1 - R0 + 2 * PAD + 1) * P + PAD;              // units the taps can touch
+    const int NQ = (L + 63) >> 6;                                 // DMA instructions per piece
+    const uint32_t plane0 = G.in_l.o0 - 3u * (uint32_t)P - 3u;    // plane start of the slice's group 0
+    const int cin_g = a.cin_g;
+
+    // window of input group g -> buffer g & 1 (units [ws, ws + 64 NQ) of each piece plane)
+    auto dma_win = [&](int g) __attribute__((always_inline)) {
+        const uint32_t src = (plane0 + (uint32_t)g * G.in_l.gs + (uint32_t)ws) * 16u;
+        uint4* dst = lds + 2 * A_U + (g & 1) * WBUF;
+        for (int i = wave; i < 3 * NQ; i += NW) {
+            const int pc = i / NQ, j = i - pc * NQ;
+            const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(G.in + (size_t)pc * G.in_ps), (short)0, (int)G.in_ps, 0x00020000);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(dst + pc * WMAX + 64 * j), 16,
+                                                     src + (uint32_t)(64 * j + lane) * 16u, 0, 0, 0);
+        }
+    };
+    // weights: one buffer resource per chunk, the unit's row offset in soffset, lane * 16 in voffset
+    const uint32_t lane16 = (uint32_t)lane * 16u;
+    auto dma_a_unit = [&](int c, int buf, int u) __attribute__((always_inline)) {
+        uint4* As = lds + buf * A_U;
+        const int unit0 = (wave * A_PW + u) * 64;
+        const int pg = unit0 / MT, m = unit0 - pg * MT;
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(G.wt + (size_t)c * 12 * a.Mpad * 16), (short)0, (int)0x7fffffff, 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(As + unit0), 16, lane16,
+                                                 (int)((uint32_t)(pg * a.Mpad + m0 + m) * 16u), 0, 0);
+    };
+    auto dma_a = [&](int c, int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < A_PW; ++u) dma_a_unit(c, buf, u);
+    };
+
+    // ---- per-lane B fragment addresses: lane (k-group gi = lane >> 4, pixel lane & 15 of block j)
+    const int gi = lane >> 4;
+    uint32_t bbase[TN];  // LDS byte address of the lane's pixel unit (window buffer 0, piece 0)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int p = min(p0 + wp0 + 16 * j + (lane & 15), a.npix - 1);  // past the end: any window unit
+        const int n = p / HW, r = p - n * HW, y = r / W, x = r - y * W;
+        const int wpos = (3 + n * (H + 3) + y) * P + 3 + x - ws;
+        bbase[j] = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + 2 * A_U + wpos);
+    }
+    // pair of this lane's k-group in a chunk: q = 4c + gi -> (group g, tap t), advanced by 4 per chunk
+    int pg_g = 0, pg_t = gi;  // chunk 0
+    auto pair_off = [&]() __attribute__((always_inline)) -> uint32_t {
+        const int g = min(pg_g, cin_g - 1);  // padded pairs past the last group: its data (weights 0)
+        const int ky = pg_t / KS;
+        const int shift = (ky - PAD) * P + (pg_t - ky * KS - PAD);
+        return (uint32_t)((g & 1) * WBUF * 16 + shift * 16);
+    };
+    auto advance = [&]() __attribute__((always_inline)) {
+        pg_t += 4;
+        if (pg_t >= TAPS) {
+            pg_t -= TAPS;
+            ++pg_g;
+        }
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    i32x4 fa[3][TM], fb[3][TN];
+    constexpr int PA[6] = {0, 0, 0, 1, 2, 1};
+    constexpr int PB[6] = {2, 0, 1, 0, 0, 1};
+    constexpr int NB = TM * TN;
+    constexpr int TMN = TM + TN;
+    const int a16 = (lane >> 4) * MT + wm0 + (lane & 15);
+    auto la = [&](int buf) __attribute__((always_inline)) {
+        return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * A_U + a16);
+    };
+    // refill group g (0: A0 B2, 1: B0 A2, 2: B1 A1), read r of TMN; B addresses of the chunk in bq
+    auto rd = [&](int g, int r, uint32_t abase, const uint32_t (&bq)[TN]) __attribute__((always_inline)) {
+        const bool isA = g == 0 ? r < TM : r >= TN;
+        const int k = g == 0 ? (r < TM ? r : r - TM) : (r < TN ? r : r - TN);
+        const int pc = g == 0 ? (isA ? 0 : 2) : g == 1 ? (isA ? 2 : 0) : 1;
+        if (isA)
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[pc][k]) : "v"(abase), "i"((pc * 4 * MT + 16 * k) * 16));
+        else
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[pc][k]) : "v"(bq[k]), "i"(pc * WMAX * 16));
+    };
+    auto mf = [&](int t, int q) __attribute__((always_inline)) {
+        const int i = q / TN, j = q % TN;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[PA[t]][i]),
+                                                            __builtin_bit_cast(bf16x8, fb[PB[t]][j]), acc[i][j], 0,
+                                                            0, 0);
+    };
+    auto fence_all = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[pc][i]));
+#pragma unroll
+            for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(fb[pc][j]));
+        }
+    };
+
+    // ---- prologue: windows of groups 0 and 1, weight stages of chunks 0 and 1
+    dma_win(0);
+    if (cin_g > 1) dma_win(1);
+    dma_a(0, 0);
+    dma_a(min(1, nK - 1), 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // both windows and both stages landed everywhere
+    uint32_t bcur[TN], bnxt[TN];
+    {
+        const uint32_t off = pair_off();
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bnxt[j] = bbase[j] + off;  // chunk 0
+        const uint32_t a0 = la(0);
+#pragma unroll
+        for (int r = 0; r < TMN; ++r) rd(0, r, a0, bnxt);
+#pragma unroll
+        for (int r = 0; r < TMN; ++r) rd(1, r, a0, bnxt);
+    }
+    // group whose last chunk comes next, and that chunk: its buffer is refilled after that barrier
+    int end_g = 0;
+    int end_c = (TAPS - 1) / 4;
+    for (int c = 0; c < nK; ++c) {
+        const int buf = c & 1;
+        const uint32_t a_cur = la(buf), a_nxt = la(buf ^ 1);
+        const int c2 = min(c + 2, nK - 1);  // past the end: a harmless reload of the last chunk
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bcur[j] = bnxt[j];
+        advance();  // (pg_g, pg_t) -> chunk c + 1
+        {
+            const uint32_t off = pair_off();
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bnxt[j] = bbase[j] + off;
+        }
+        // block 0 (needs R0): R2 of this chunk interleaved
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TMN > 15 ? 15 : TMN) : "memory");
+        fence_all();
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            mf(0, q);
+#pragma unroll
+            for (int r = q * TMN / NB; r < (q + 1) * TMN / NB; ++r) rd(2, r, a_cur, bcur);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // block 1 (needs R1)
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TMN > 15 ? 15 : TMN) : "memory");
+        fence_all();
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            mf(1, q);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // block 2 (needs R2)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        fence_all();
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            mf(2, q);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // this weight stage and every fragment of chunk c read by all; the next stage (and any
+        // window DMA'd since the previous barrier) landed.  The vmcnt(0) is explicit: the
+        // compiler does not count LDS-DMA as LDS writes at a workgroup barrier (it emitted a
+        // bare s_barrier here), and the fragment reads are inline asm it cannot see
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);
+        if (c == end_c) {  // group end_g is read for the last time: its buffer takes group end_g + 2
+            if (end_g + 2 < cin_g) dma_win(end_g + 2);
+            ++end_g;
+            end_c = (end_g * TAPS + TAPS - 1) / 4;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // blocks 3-5: R0 (block 3) and R1 (block 5) of the next chunk, weight DMA of chunk c2
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            mf(3, q);
+            constexpr int N3 = TMN + 1;
+#pragma unroll
+            for (int o = q * N3 / NB; o < (q + 1) * N3 / NB; ++o) {
+                if (o < TMN) rd(0, o, a_nxt, bnxt);
+                else dma_a_unit(c2, buf, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            mf(4, q);
+            constexpr int N4 = A_PW - 2;
+#pragma unroll
+            for (int o = q * N4 / NB; o < (q + 1) * N4 / NB; ++o) dma_a_unit(c2, buf, 1 + o);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            mf(5, q);
+            constexpr int N5 = TMN + 1;
+#pragma unroll
+            for (int o = q * N5 / NB; o < (q + 1) * N5 / NB; ++o) {
+                if (o < TMN) rd(1, o, a_nxt, bnxt);
+                else dma_a_unit(c2, buf, A_PW - 1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the last (unused) reads / loads landed
+    fence_all();
+
+    // ---- epilogue (conv_x6's, whole tiles): bias + ReLU, X6 / X6P slices or fp32 NCHW
+    const int cout8 = (G.cout + 7) & ~7;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int p = p0 + wp0 + j * 16 + (lane & 15);
+        if (p >= a.npix) continue;
+        const int n = p / HW;
+        const int rem = p - n * HW;
+        const int y = rem / W, x = rem - y * W;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int ml = wm0 + i * 16 + 4 * (lane >> 4);  // first of 4 consecutive channels
+            const int mq = m0 + ml;
+            float v[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                v[t] = acc[i][j][t] + s_bias[ml + t];
+                if (G.relu) v[t] = fmaxf(v[t], 0.f);
+            }
+            if (G.out_f32) {
+                float* ob = static_cast<float*>(G.out) + ((size_t)n * G.out_c + G.out_off) * HW + rem;
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if (mq + t < G.cout) ob[(size_t)(mq + t) * HW] = v[t];
+            } else if (mq < cout8) {
+                const int grp = mq >> 3, half = (mq >> 2) & 1;
+                store4_x6(static_cast<uint8_t*>(G.out) + (size_t)x6_unit(G.out_l, n, grp, y, x) * 16 + half * 8,
+                          G.out_ps, v);
+                if (G.out2)
+                    store4_x6(static_cast<uint8_t*>(G.out2) + (size_t)x6_unit(G.out2_l, n, grp, y, x) * 16 + half * 8,
+                              G.out2_ps, v);
+            }
+        }
+    }
+}
+
+// weights [cout][cin][ks][ks] (fp32, physical input channel order) -> X6 chunks in pair order:
+// chunk c, k-group gi = pair q = 4c + gi = (group q / taps, tap q % taps); pairs past the last
+// group are zero.  Same unit format as x6_pack_weights ([chunk][piece][4][Mpad][8] bf16).
+void x6_pack_weights_pairs(const float* w, int cout, int cin, int ks, int Mpad, int* nK_out,
+                           std::vector<uint16_t>& out) {
+    const int taps = ks * ks;
+    const int cin_g = (cin + 7) / 8;
+    const int nK = (cin_g * taps + 3) / 4;
+    *nK_out = nK;
+    out.assign((size_t)nK * 12 * Mpad * 8, 0);
+    auto rne = [](float x) -> uint32_t {
+        uint32_t u;
+        std::memcpy(&u, &x, 4);
+        u += 0x7fffu + ((u >> 16) & 1u);
+        return u >> 16;
+    };
+    auto f = [](uint32_t h) {
+        const uint32_t u = h << 16;
+        float x;
+        std::memcpy(&x, &u, 4);
+        return x;
+    };
+    for (int c = 0; c < nK; ++c)
+        for (int gi = 0; gi < 4; ++gi) {
+            const int q = 4 * c + gi, grp = q / taps, tap = q % taps;
+            if (grp >= cin_g) continue;
+            for (int m = 0; m < cout; ++m)
+                for (int e = 0; e < 8; ++e) {
+                    const int ch = grp * 8 + e;
+                    if (ch >= cin) continue;
+                    const float x = w[((size_t)m * cin + ch) * taps + tap];
+                    const uint32_t h0 = rne(x);
+                    const float r = x - f(h0);
+                    const uint32_t h1 = rne(r);
+                    const uint32_t h2 = rne(r - f(h1));
+                    const uint32_t hs[3] = {h0, h1, h2};
+                    for (int pc = 0; pc < 3; ++pc)
+                        out[(((size_t)c * 12 + pc * 4 + gi) * Mpad + m) * 8 + e] = (uint16_t)hs[pc];
+                }
+        }
+}
+
+constexpr int kWinMax = 768;  // window units per (piece, group): 17 padded rows of a 41-wide map
+
+// largest window (units) a tile of PT pixels needs on an N x H x W batch, 7x7
+int conv_win_units(int N, int H, int W, int pt) {
+    const int HW = H * W, P = W + 3, npix = N * HW;
+    int worst = 0;
+    for (int p0 = 0; p0 < npix; p0 += pt) {
+        const int p1 = std::min(p0 + pt, npix) - 1;
+        auto prow = [&](int p) { return 3 + (p / HW) * (H + 3) + (p % HW) / W; };
+        worst = std::max(worst, (prow(p1) - prow(p0) + 7) * P + 3);
+    }
+    return worst;
+}
+
+bool conv_win_fits(int N, int H, int W) { return conv_win_units(N, H, W, 256) <= kWinMax; }
+
+void launch_conv_win_x6(const X6Args& a, hipStream_t st) {
+    if (a.ks != 7 || a.small || a.pool || a.Mpad % 128 || !conv_win_fits(a.N, a.H, a.W))
+        throw std::invalid_argument("conv_win_x6: unsupported layer");
+    const int tiles = (a.Mpad / 128) * ((a.npix + 255) / 256) * a.ngroups;
+    hipLaunchKernelGGL((conv_win_x6<128, 256, 7, kWinMax>), dim3(tiles), dim3(512), 0, st, a);
+}
+
+}  // namespace opose

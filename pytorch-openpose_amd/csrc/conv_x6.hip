@@ -24,85 +24,33 @@
 //   group slice of a wider buffer (the CPM concat), or fp32 NCHW for the network outputs.
 #include <cstdlib>
 #include <cstring>
-#include <type_traits>
 #include <stdexcept>
 #include <vector>
 
 #include "common.h"
 #include "kernels.h"
-
-// Compile-time timing ablations of the 16x16x32 main loop (0 in every shipped build; results
-// are wrong when set): 1 no im2col DMA, 2 no weight DMA, 8 no LDS fragment reads, 16 barrier
-// without the vmcnt(0) DMA wait, 32 no barrier.  Built by scripts/build_ablation.sh.
-#ifndef OPOSE_X6_ABL
-#define OPOSE_X6_ABL 0
-#endif
+#include "x6.h"
 
 namespace opose {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-namespace {
-
-constexpr int x6_waves(int mt, int pt) { return mt * pt >= 32768 ? 8 : 4; }
-
-__device__ __forceinline__ uint32_t bf16_rne(float x) {
-    uint32_t u = __float_as_uint(x);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return u >> 16;
-}
-
-// x -> three bf16 pieces, x0 + x1 + x2 == x exactly (each remainder is exact by Sterbenz)
-__device__ __forceinline__ void split3(float x, uint32_t& h0, uint32_t& h1, uint32_t& h2) {
-    h0 = bf16_rne(x);
-    const float r = x - __uint_as_float(h0 << 16);
-    h1 = bf16_rne(r);
-    const float r2 = r - __uint_as_float(h1 << 16);
-    h2 = bf16_rne(r2);
-}
-
-__device__ __forceinline__ float join3(uint32_t h0, uint32_t h1, uint32_t h2) {
-    return (__uint_as_float(h0 << 16) + __uint_as_float(h1 << 16)) + __uint_as_float(h2 << 16);
-}
-
-// write 4 consecutive channels (4hk .. 4hk+3 of a group) of one pixel, split, into the 3 planes
-__device__ __forceinline__ void store4_x6(uint8_t* unit, uint32_t ps, const float (&v)[4]) {
-    uint32_t h[3][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) split3(v[t], h[0][t], h[1][t], h[2][t]);
-#pragma unroll
-    for (int pc = 0; pc < 3; ++pc) {
-        uint2 w;
-        w.x = h[pc][0] | (h[pc][1] << 16);
-        w.y = h[pc][2] | (h[pc][3] << 16);
-        *reinterpret_cast<uint2*>(unit + (size_t)pc * ps) = w;
-    }
-}
-
-}  // namespace
-
-// MODE 0: two-wait chunk loop (A/B reference); 1: pipelined, v_mfma_f32_32x32x16_bf16;
-// 2: pipelined, v_mfma_f32_16x16x32_bf16 (one k-step per chunk); 3: as 2 with the im2col
-// fragments loaded straight from global memory into registers (LDS holds only the weights)
-template <int MT, int PT, bool SMALL, int KS, int MODE>
+// Main loop: v_mfma_f32_16x16x32_bf16, one k-step (32 k) per chunk, refill-after-last-use
+// fragment schedule pinned by sched_barrier (see below).  Measured and dropped:
+// a two-wait loop, the 32x32x16 pipelined loop, and im2col fragments loaded straight into
+// registers (same speed, LDS for the weights only).
+template <int MT, int PT, bool SMALL, int KS>
 __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int ks = KS ? KS : a.ks;
     const int taps = ks * ks;
-    // waves along M: 8-wave tiles and 64x256 (four 64x64 waves, the 128x256 tile's per-wave
-    // shape for M = 64 layers) one per 64 rows; the other 4-wave tiles 2 x 2
-    constexpr int NW = x6_waves(MT, PT), NWM = (NW == 8 || PT == 4 * MT) ? MT / 64 : 2, NWP = NW / NWM;
+    // waves along M: 8-wave tiles one per 64 rows; the 4-wave tiles 2 x 2
+    constexpr int NW = x6_waves(MT, PT), NWM = NW == 8 ? MT / 64 : 2, NWP = NW / NWM;
     constexpr int WM = MT / NWM, WP = PT / NWP;
-    constexpr bool PIPE = MODE >= 1, S16 = MODE >= 2, BREG = MODE == 3;
-    constexpr int MB = S16 ? 16 : 32;            // MFMA block (rows = pixels)
+    constexpr int MB = 16;                       // MFMA block (rows = pixels)
     constexpr int TM = WM / MB, TN = WP / MB;
     constexpr int ACC_N = MB * MB / 64;          // accumulator registers per block
-    using AccT = typename std::conditional<S16, f32x4, floatx16>::type;
+    using AccT = f32x4;
     constexpr int PJ = PT / 64;                  // 64-pixel runs per tile
-    constexpr int A_U = 12 * MT, B_U = BREG ? 0 : 12 * PT;  // 16-byte units per stage (BREG: no B tile)
+    constexpr int A_U = 12 * MT, B_U = 12 * PT;  // 16-byte units per stage
     constexpr int A_PW = A_U / 64 / NW;          // A DMA instructions per wave per chunk
     constexpr int WPJ = NW / PJ;                 // waves sharing one pixel run
     constexpr int B_PW = 12 / WPJ;               // B DMA instructions per wave per chunk
@@ -115,7 +63,6 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int l31 = lane & 31, hk = lane >> 5;
     const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
     const int nK = a.nK;
     const int HW = a.H * a.W;
@@ -164,7 +111,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         if (tid < MT) s_bias[tid] = (m0 + tid < G.cout) ? G.bias[m0 + tid] : 0.f;
 
         // the lane's im2col pixel (run jw): byte offset of its unit in group 0, plane 0
-        const uint8_t* in_base = G.in + (size_t)G.in_goff * HW * 16;
+        const uint8_t* in_base = G.in + (size_t)G.in_l.o0 * 16;
         int py, px;
         uint32_t pbase;
         {
@@ -172,9 +119,10 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             const bool v = p < a.npix;
             int n, r;
             decode(v ? p : 0, n, r);
-            py = v ? r / a.W : -100000;
-            px = r - (r / a.W) * a.W;
-            pbase = (uint32_t)(n * G.in_cg * HW + r) * 16u;
+            const int y = r / a.W;
+            px = r - y * a.W;
+            py = v ? y : -100000;
+            pbase = (n * G.in_l.fs + (uint32_t)y * G.in_l.rs + (uint32_t)px) * 16u;
         }
 
         AccT acc[TM][TN];
@@ -190,7 +138,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             const int dy = ky - a.pad, dx = tap - ky * ks - a.pad;
             const int iy = py + dy, ix = px + dx;
             const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-            return ok ? pbase + (uint32_t)((dy * a.W + dx) * 16) : 0x80000000u;  // >= num_records -> 0
+            return ok ? pbase + (uint32_t)((dy * (int)G.in_l.rs + dx) * 16) : 0x80000000u;  // >= num_records -> 0
         };
         // im2col DMA of chunk c, unit u of this wave ((piece, group) row pg0 + u * WPJ) into stage buf;
         // voff / cb: the chunk's tap offset and channel block (b_prep).  One buffer resource per
@@ -208,7 +156,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             }
             return r;
         };
-        const uint32_t grp_bytes = (uint32_t)HW * 16u;
+        const uint32_t grp_bytes = G.in_l.gs * 16u;
         auto dma_b_unit = [&](int c, const BPrep& bp, int buf, int u) __attribute__((always_inline)) {
             uint4* Bs = lds + buf * STAGE_U + A_U;
             const int pg = pg0 + u * WPJ;
@@ -248,231 +196,8 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             for (int u = 0; u < A_PW; ++u) dma_a_unit(c, buf, u);
         };
 
-        i32x4 fa[S16 ? 1 : 2][3][TM], fb[S16 ? 1 : 2][3][TN];
-        auto lds_a = [&](int buf) __attribute__((always_inline)) {
-            return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * STAGE_U + hk * MT + wm0 + l31);
-        };
-        auto lds_b = [&](int buf) __attribute__((always_inline)) {
-            return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * STAGE_U + A_U + hk * PT + wp0 + l31);
-        };
-        // fragments of k-step s (16 k) of the stage at a_lds / b_lds
-        auto read_step = [&](int s, uint32_t a_lds, uint32_t b_lds) __attribute__((always_inline)) {
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-                    asm volatile("ds_read_b128 %0, %1 offset:%2"
-                                 : "=v"(fa[s][pc][i])
-                                 : "v"(a_lds), "i"(((pc * 4 + 2 * s) * MT + 32 * i) * 16));
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    asm volatile("ds_read_b128 %0, %1 offset:%2"
-                                 : "=v"(fb[s][pc][j])
-                                 : "v"(b_lds), "i"(((pc * 4 + 2 * s) * PT + 32 * j) * 16));
-            }
-        };
-        // the fragments of k-step s are in registers: make later uses depend on the wait
-        auto fence_step = [&](int s) __attribute__((always_inline)) {
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[s][pc][i]));
-#pragma unroll
-                for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(fb[s][pc][j]));
-            }
-        };
-        auto mfma_step = [&](int s) __attribute__((always_inline)) {
-            // small terms first: (2,0) (1,1) (0,2) (1,0) (0,1) (0,0)
-            constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
-            constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-            for (int t = 0; t < 6; ++t)
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        if constexpr (!S16)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                                __builtin_bit_cast(bf16x8, fa[s][PA[t]][i]),
-                                __builtin_bit_cast(bf16x8, fb[s][PB[t]][j]), acc[i][j], 0, 0, 0);
-                    }
-        };
-
-        if constexpr (BREG) {
-            // Weights through LDS (LDS-DMA, two stages, one barrier per chunk), im2col fragments
-            // straight from global memory into registers: lane l loads the 16-byte unit of pixel
-            // (l & 15) of each 16-pixel block, channel group (l >> 4) of the chunk, per piece --
-            // exactly its B fragment -- one chunk ahead into the other of two register sets.
-            // The two M-halves of the workgroup load the same units (L1 hits); LDS read bytes halve
-            // and the im2col LDS-DMA disappears.
-            constexpr int PA[6] = {0, 0, 0, 1, 2, 1};
-            constexpr int PB[6] = {2, 0, 1, 0, 0, 1};
-            constexpr int NB = TM * TN;
-            constexpr int NBL = 3 * TN;  // B loads per chunk
-            const int a16 = (lane >> 4) * MT + wm0 + (lane & 15);
-            auto la = [&](int buf) __attribute__((always_inline)) {
-                return (uint32_t)(uintptr_t)(lds_ptr_t)(lds + buf * STAGE_U + a16);
-            };
-            // A refill groups: 0 = A0 (after block 2), 1 = A2 (after block 4), 2 = A1 (next block 0)
-            auto rda = [&](int g, int k, uint32_t abase) __attribute__((always_inline)) {
-                const int pc = g == 0 ? 0 : g == 1 ? 2 : 1;
-                asm volatile("ds_read_b128 %0, %1 offset:%2"
-                             : "=v"(fa[0][pc][k])
-                             : "v"(abase), "i"((pc * 4 * MT + 16 * k) * 16));
-            };
-            // per-lane pixel of each block j: frame-relative row / column, byte offset of its unit
-            int by[TN], bx[TN];
-            uint32_t bbase[TN];
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int p = p0 + wp0 + 16 * j + (lane & 15);
-                const bool v = p < a.npix;
-                int n, r;
-                decode(v ? p : 0, n, r);
-                by[j] = v ? r / a.W : -100000;
-                bx[j] = r - (r / a.W) * a.W;
-                bbase[j] = (uint32_t)(n * G.in_cg * HW + r) * 16u;
-            }
-            const int gl = lane >> 4;
-            __amdgpu_buffer_rsrc_t brs[3];
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc)
-                brs[pc] = __builtin_amdgcn_make_buffer_rsrc((void*)(in_base + (size_t)pc * G.in_ps), (short)0,
-                                                             (int)0x80000000u, 0x00020000);
-            i32x4 fbr[2][3][TN];
-            // voffset of block j for chunk c (tap validity -> out-of-range marker), soffset = the
-            // chunk's channel-block offset
-            struct BOff {
-                uint32_t v[TN];
-                int s;
-            };
-            auto boff = [&](int c) __attribute__((always_inline)) -> BOff {
-                BOff o;
-                int tap, cb = 0, gi;
-                if constexpr (SMALL) {
-                    tap = min(c * 4 + gl, taps - 1);  // padded taps: weights are 0
-                    gi = 0;
-                } else {
-                    cb = c / taps;
-                    tap = c - cb * taps;
-                    gi = min(cb * 4 + gl, a.cin_g - 1) - cb * 4;  // padded groups: valid data, weights 0
-                }
-                const int ky = tap / ks;
-                const int dy = ky - a.pad, dx = tap - ky * ks - a.pad;
-                const uint32_t d = (uint32_t)((dy * a.W + dx) * 16) + (uint32_t)gi * grp_bytes;
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const bool ok = (unsigned)(by[j] + dy) < (unsigned)a.H && (unsigned)(bx[j] + dx) < (unsigned)a.W;
-                    o.v[j] = ok ? bbase[j] + d : 0x80000000u;
-                }
-                o.s = (int)((uint32_t)(cb * 4) * grp_bytes);
-                return o;
-            };
-            auto ldb = [&](int set, int i, const BOff& o) __attribute__((always_inline)) {
-                const int pc = (i / TN + 2) % 3, j = i % TN;  // pieces in order of first use: 2, 0, 1
-                fbr[set][pc][j] = __builtin_amdgcn_raw_buffer_load_b128(brs[pc], o.v[j], o.s, 0);
-            };
-            auto fence_a = [&]() __attribute__((always_inline)) {
-#pragma unroll
-                for (int pc = 0; pc < 3; ++pc)
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[0][pc][i]));
-            };
-            // one chunk with B register set SET: blocks 0-2, barrier, blocks 3-5
-            auto chunk = [&](int c, auto set_c) __attribute__((always_inline)) {
-                constexpr int SET = decltype(set_c)::value;
-                const int buf = (c - c_begin) & 1;
-                const uint32_t a_cur = la(buf), a_nxt = la(buf ^ 1);
-                const int c1 = min(c + 1, c_end - 1);  // past the end: harmless reloads
-                const int c2 = min(c + 2, c_end - 1);
-                const BOff ob = boff(c1);
-                auto mf = [&](int t, int q) __attribute__((always_inline)) {
-                    const int i = q / TN, j = q % TN;
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        __builtin_bit_cast(bf16x8, fa[0][PA[t]][i]), __builtin_bit_cast(bf16x8, fbr[SET][PB[t]][j]),
-                        acc[i][j], 0, 0, 0);
-                };
-                asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TM > 15 ? 15 : TM) : "memory");  // A0 (R0)
-                fence_a();
-                __builtin_amdgcn_sched_barrier(0);
-                // block 0: A1 refill of this chunk (R2) + the next chunk's B loads (first part)
-                constexpr int N0 = TM + NBL / 2;
-#pragma unroll
-                for (int q = 0; q < NB; ++q) {
-                    mf(0, q);
-#pragma unroll
-                    for (int o = q * N0 / NB; o < (q + 1) * N0 / NB; ++o) {
-                        if (o < TM) rda(2, o, a_cur);
-                        else ldb(SET ^ 1, o - TM, ob);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                constexpr int N1 = NBL - NBL / 2;
-#pragma unroll
-                for (int q = 0; q < NB; ++q) {
-                    mf(1, q);
-#pragma unroll
-                    for (int o = q * N1 / NB; o < (q + 1) * N1 / NB; ++o) ldb(SET ^ 1, NBL / 2 + o, ob);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-#pragma unroll
-                for (int q = 0; q < NB; ++q) {
-                    mf(2, q);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                // this stage read by every wave (R2 waited); the next A stage landed: its DMA is
-                // older than the NBL B loads just issued
-                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(NBL) : "memory");
-                fence_a();
-                __builtin_amdgcn_s_barrier();
-                __builtin_amdgcn_sched_barrier(0);
-                // blocks 3-5: A0 refill (R0) in block 3, A DMA of chunk c2 in block 4, A2 (R1) in 5
-#pragma unroll
-                for (int q = 0; q < NB; ++q) {
-                    mf(3, q);
-#pragma unroll
-                    for (int o = q * TM / NB; o < (q + 1) * TM / NB; ++o) rda(0, o, a_nxt);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-#pragma unroll
-                for (int q = 0; q < NB; ++q) {
-                    mf(4, q);
-#pragma unroll
-                    for (int o = q * A_PW / NB; o < (q + 1) * A_PW / NB; ++o) dma_a_unit(c2, buf, o);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-#pragma unroll
-                for (int q = 0; q < NB; ++q) {
-                    mf(5, q);
-#pragma unroll
-                    for (int o = q * TM / NB; o < (q + 1) * TM / NB; ++o) rda(1, o, a_nxt);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            };
-            // prologue: A stage 0 landed, A0 / A2 fragments of the first chunk issued, its B loads
-            dma_a(c_begin, 0);
-            {
-                const BOff o0 = boff(c_begin);
-#pragma unroll
-                for (int i = 0; i < NBL; ++i) ldb(0, i, o0);
-            }
-            __syncthreads();
-            {
-                const uint32_t a0 = la(0);
-#pragma unroll
-                for (int k = 0; k < TM; ++k) rda(0, k, a0);
-#pragma unroll
-                for (int k = 0; k < TM; ++k) rda(1, k, a0);
-                dma_a(min(c_begin + 1, c_end - 1), 1);
-            }
-            for (int c = c_begin; c < c_end; c += 2) {
-                chunk(c, std::integral_constant<int, 0>());
-                if (c + 1 < c_end) chunk(c + 1, std::integral_constant<int, 1>());
-            }
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the last (unused) loads landed
-            fence_a();
-        } else if constexpr (S16) {
-
+        i32x4 fa[1][3][TM], fb[1][3][TN];
+        {
             // 16x16x32 MFMAs: a chunk (32 k) is one k-step.  Lane l holds row / pixel (l & 15) and
             // the k-group (l >> 4) of its 16-row block; the LDS layout is the same [piece][group][row]
             // unit array (ds_read_b128's 16-lane phases hit 4 rows of each of 4 groups: conflict free).
@@ -499,7 +224,6 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             };
             // refill group g (0: A0 B2, 1: B0 A2, 2: B1 A1), read r of TMN
             auto rd = [&](int g, int r, uint32_t abase, uint32_t bbase) __attribute__((always_inline)) {
-                if constexpr ((OPOSE_X6_ABL & 8) != 0) return;
                 const bool isA = g == 0 ? r < TM : r >= TN;
                 const int k = g == 0 ? (r < TM ? r : r - TM) : (r < TN ? r : r - TN);
                 const int pc = g == 0 ? (isA ? 0 : 2) : g == 1 ? (isA ? 2 : 0) : 1;
@@ -529,6 +253,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             };
             dma_a(c_begin, 0);
             dma_b(c_begin, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             {
                 const uint32_t a0 = la(0), b0 = lb(0);
@@ -575,20 +300,16 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
                     mf(2, q);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                if constexpr ((OPOSE_X6_ABL & 48) == 0) {
-                    __syncthreads();  // this stage read by all; the next stage landed (vmcnt(0) first)
-                } else if constexpr ((OPOSE_X6_ABL & 32) == 0) {
-                    __builtin_amdgcn_s_barrier();
-                }
+                // this stage read by all; the next stage landed (explicit vmcnt(0): the compiler's
+                // barrier fence does not reliably count LDS-DMA, see conv_win.hip)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
                 __builtin_amdgcn_sched_barrier(0);
                 // blocks 3-5: R0 (block 3) and R1 (block 5) of the next chunk, DMA of chunk c2
                 constexpr int D3 = NDA / 3, D4 = 2 * NDA / 3;
                 auto dma_op = [&](int d) __attribute__((always_inline)) {
-                    if (d < A_PW) {
-                        if constexpr (!(OPOSE_X6_ABL & 2)) dma_a_unit(c2, buf, d);
-                    } else {
-                        if constexpr (!(OPOSE_X6_ABL & 1)) dma_b_unit(c2, bp2, buf, d - A_PW);
-                    }
+                    if (d < A_PW) dma_a_unit(c2, buf, d);
+                    else dma_b_unit(c2, bp2, buf, d - A_PW);
                 };
 #pragma unroll
                 for (int q = 0; q < NB; ++q) {
@@ -623,102 +344,6 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last (unused) reads landed
             fence_all();
-        } else if constexpr (PIPE) {
-            // Software-pipelined chunk loop, one barrier per chunk, placed between the two k-steps:
-            //   step 0: 6*TM*TN MFMAs on the fragments of k-step 0, with the LDS reads of k-step 1
-            //           interleaved (one per MFMA gap);
-            //   wait for them, vmcnt(0) + barrier: every wave has read this stage, and the next
-            //           stage (its DMA issued one chunk earlier) has landed everywhere;
-            //   step 1: MFMAs of k-step 1, interleaved with the reads of the next chunk's k-step 0
-            //           and then the DMA of the chunk after it into this (now free) stage.
-            // sched_barrier pins the order: left alone the compiler sinks the MFMAs below the
-            // waits, exposing the LDS latency twice per chunk.
-            constexpr int NMF = 6 * TM * TN;   // MFMAs per k-step
-            constexpr int NRD = 3 * (TM + TN); // ds_read_b128 per k-step
-            constexpr int NDA = A_PW + B_PW;   // LDS-DMA instructions per chunk
-            constexpr int PA[6] = {2, 1, 0, 1, 0, 0};  // small terms first
-            constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
-            auto read_one = [&](int s, int r, uint32_t a_lds, uint32_t b_lds) __attribute__((always_inline)) {
-                const int pc = r / (TM + TN), k = r % (TM + TN);
-                if (k < TM)
-                    asm volatile("ds_read_b128 %0, %1 offset:%2"
-                                 : "=v"(fa[s][pc][k])
-                                 : "v"(a_lds), "i"(((pc * 4 + 2 * s) * MT + 32 * k) * 16));
-                else
-                    asm volatile("ds_read_b128 %0, %1 offset:%2"
-                                 : "=v"(fb[s][pc][k - TM])
-                                 : "v"(b_lds), "i"(((pc * 4 + 2 * s) * PT + 32 * (k - TM)) * 16));
-            };
-            auto mfma_one = [&](int s, int q) __attribute__((always_inline)) {
-                const int t = q / (TM * TN), i = (q / TN) % TM, j = q % TN;
-                if constexpr (!S16)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[s][PA[t]][i]),
-                                                                        __builtin_bit_cast(bf16x8, fb[s][PB[t]][j]),
-                                                                        acc[i][j], 0, 0, 0);
-            };
-            dma_a(c_begin, 0);
-            dma_b(c_begin, 0);
-            __syncthreads();
-            read_step(0, lds_a(0), lds_b(0));
-            {
-                const int cn = min(c_begin + 1, c_end - 1);
-                dma_a(cn, 1);
-                dma_b(cn, 1);
-            }
-            for (int c = c_begin; c < c_end; ++c) {
-                const int buf = (c - c_begin) & 1;
-                const uint32_t a_cur = lds_a(buf), b_cur = lds_b(buf);
-                const uint32_t a_nxt = lds_a(buf ^ 1), b_nxt = lds_b(buf ^ 1);
-                const int c2 = min(c + 2, c_end - 1);  // past the end: a harmless reload of the last chunk
-                const BPrep bp2 = b_prep(c2);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                fence_step(0);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int q = 0; q < NMF; ++q) {
-                    mfma_one(0, q);
-#pragma unroll
-                    for (int r = q * NRD / NMF; r < (q + 1) * NRD / NMF; ++r) read_one(1, r, a_cur, b_cur);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                fence_step(1);
-                __syncthreads();  // this stage read by all; next stage landed (vmcnt(0) first)
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int q = 0; q < NMF; ++q) {
-                    mfma_one(1, q);
-#pragma unroll
-                    for (int o = q * (NRD + NDA) / NMF; o < (q + 1) * (NRD + NDA) / NMF; ++o) {
-                        if (o < NRD) read_one(0, o, a_nxt, b_nxt);
-                        else if (o < NRD + A_PW) dma_a_unit(c2, buf, o - NRD);
-                        else dma_b_unit(c2, bp2, buf, o - NRD - A_PW);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last (unused) reads landed
-            fence_step(0);
-        } else {
-            dma_a(c_begin, 0);
-            dma_b(c_begin, 0);
-            __syncthreads();
-            for (int c = c_begin; c < c_end; ++c) {
-                const int buf = (c - c_begin) & 1;
-                const int cn = min(c + 1, c_end - 1);  // the last chunk re-loads itself into the free stage
-                const int abl = a.ablate;              // timing ablations only (opose_debug_conv_x6_time)
-                if (!(abl & 8)) read_step(0, lds_a(buf), lds_b(buf));
-                if (!(abl & 2)) dma_a(cn, buf ^ 1);
-                if (!(abl & 1)) dma_b(cn, buf ^ 1);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                fence_step(0);
-                if (!(abl & 8)) read_step(1, lds_a(buf), lds_b(buf));
-                mfma_step(0);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                fence_step(1);
-                mfma_step(1);
-                if (!(abl & 4)) __syncthreads();  // next stage landed everywhere; this stage free
-            }
         }
 
         // ---- epilogue
@@ -730,10 +355,11 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         const int cout8 = (G.cout + 7) & ~7;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const int pl = S16 ? wp0 + j * 16 + (lane & 15) : wp0 + j * 32 + l31;
+            const int pl = wp0 + j * 16 + (lane & 15);
             const int p = p0 + pl;
             auto quad_row = [&](int i, int qd) __attribute__((always_inline)) {
-                return S16 ? wm0 + i * 16 + 4 * (lane >> 4) : wm0 + i * 32 + 8 * qd + 4 * hk;
+                (void)qd;
+                return wm0 + i * 16 + 4 * (lane >> 4);
             };
             if (!whole) {
 #pragma unroll
@@ -754,6 +380,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
                 const int q = p >> 2;
                 const int n = q / HWo;
                 const int remo = q - n * HWo;
+                const int yo = remo / Wo, xo = remo - yo * Wo;
                 const bool lead = (lane & 3) == 0 && p < a.npix;
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
@@ -772,8 +399,8 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
                         }
                         if (lead && mq < cout8) {
                             const int grp = mq >> 3, half = (mq >> 2) & 1;
-                            store4_x6(static_cast<uint8_t*>(G.out) +
-                                          ((size_t)(n * G.out_c + G.out_off + grp) * HWo + remo) * 16 + half * 8,
+                            store4_x6(static_cast<uint8_t*>(G.out) + (size_t)x6_unit(G.out_l, n, grp, yo, xo) * 16 +
+                                          half * 8,
                                       G.out_ps, v);
                         }
                     }
@@ -782,6 +409,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             if (p >= a.npix) continue;
             const int n = p / HW;
             const int rem = p - n * HW;
+            const int y = rem / a.W, x = rem - y * a.W;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -803,12 +431,11 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
                         }
                     } else if (mq < cout8) {
                         const int grp = mq >> 3, half = (mq >> 2) & 1;
-                        store4_x6(static_cast<uint8_t*>(G.out) +
-                                      ((size_t)(n * G.out_c + G.out_off + grp) * HW + rem) * 16 + half * 8,
+                        store4_x6(static_cast<uint8_t*>(G.out) + (size_t)x6_unit(G.out_l, n, grp, y, x) * 16 + half * 8,
                                   G.out_ps, v);
                         if (G.out2)
-                            store4_x6(static_cast<uint8_t*>(G.out2) +
-                                          ((size_t)(n * G.out2_c + G.out2_off + grp) * HW + rem) * 16 + half * 8,
+                            store4_x6(static_cast<uint8_t*>(G.out2) + (size_t)x6_unit(G.out2_l, n, grp, y, x) * 16 +
+                                          half * 8,
                                       G.out2_ps, v);
                     }
                 }
@@ -871,12 +498,50 @@ __global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
         return;
     }
     const int grp = mg >> 3, half = (mg >> 2) & 1;
-    store4_x6(static_cast<uint8_t*>(G.out) + ((size_t)(n * G.out_c + G.out_off + grp) * HW + rem) * 16 + half * 8,
-              G.out_ps, v);
+    const int y = rem / a.W, x = rem - y * a.W;
+    store4_x6(static_cast<uint8_t*>(G.out) + (size_t)x6_unit(G.out_l, n, grp, y, x) * 16 + half * 8, G.out_ps, v);
     if (G.out2)
-        store4_x6(static_cast<uint8_t*>(G.out2) + ((size_t)(n * G.out2_c + G.out2_off + grp) * HW + rem) * 16 +
-                      half * 8,
-                  G.out2_ps, v);
+        store4_x6(static_cast<uint8_t*>(G.out2) + (size_t)x6_unit(G.out2_l, n, grp, y, x) * 16 + half * 8, G.out2_ps,
+                  v);
+}
+
+static int grid_for(size_t total) {
+    size_t b = (total + 255) / 256;
+    return (int)(b > 8192 ? 8192 : (b ? b : 1));
+}
+
+// Zero the padding units of `planes` X6P planes (common.h): the 3N + 4 rows outside the frames'
+// pixel rows and the 3 units before each of the N*H pixel rows.  One thread per padding unit.
+__global__ __launch_bounds__(256) void x6p_clear_pads_kernel(uint4* __restrict__ buf, size_t plane, int N, int H,
+                                                             int P, int planes) {
+    const int pad_rows = 3 * N + 4;
+    const size_t per_plane = (size_t)pad_rows * P + (size_t)N * H * 3;
+    const size_t total = per_plane * planes;
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const size_t pl = e / per_plane;
+        size_t u = e - pl * per_plane;
+        size_t unit;
+        if (u < (size_t)pad_rows * P) {  // whole padding rows: 3 before frame 0, 3 after each frame, 1 extra
+            const int pr = (int)(u / P), c = (int)(u - (size_t)pr * P);
+            const int row = pr < 3 ? pr : 3 + ((pr - 3) / 3) * (H + 3) + H + (pr - 3) % 3;
+            unit = (size_t)(pr >= 3 * N + 3 ? 3 + N * (H + 3) + (pr - 3 * N - 3) : row) * P + c;
+        } else {  // the 3 units at the start of a pixel row
+            u -= (size_t)pad_rows * P;
+            const int pr = (int)(u / 3), c = (int)(u - (size_t)pr * 3);
+            const int n = pr / H, y = pr - n * H;
+            unit = (size_t)(3 + n * (H + 3) + y) * P + c;
+        }
+        buf[pl * plane + unit] = z;
+    }
+}
+
+void launch_x6p_clear_pads(uint8_t* buf, int planes, int N, int H, int W, hipStream_t st) {
+    const int P = W + 3;
+    const size_t plane = (size_t)(N * (H + 3) + 4) * P;
+    const size_t pads = ((size_t)(3 * N + 4) * P + (size_t)N * H * 3) * planes;
+    hipLaunchKernelGGL(x6p_clear_pads_kernel, dim3(grid_for(pads)), dim3(256), 0, st, reinterpret_cast<uint4*>(buf),
+                       plane, N, H, P, planes);
 }
 
 // fp32 NCHW channels [coff, coff + C) of cstride -> X6 groups [goff, goff + ceil(C/8)) of cg
@@ -1029,39 +694,19 @@ void x6_pack_weights(const float* w, int cout, int cin, int ks, int Mpad, int* n
         }
 }
 
-// main-loop variant: OPOSE_X6_MODE = 0 (two-wait loop), 1 (pipelined 32x32x16), 2 (pipelined
-// 16x16x32); default 2
-static int x6_mode() {
-    static const int m = [] {
-        const char* e = getenv("OPOSE_X6_MODE");
-        return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 2;
-    }();
-    return m;
-}
-
-template <int MT, int PT, int MODE>
-static void launch_x6_tile_m(const X6Args& a, hipStream_t st) {
-    const dim3 blk(64 * x6_waves(MT, PT));
-    if (a.small != 0)
-        hipLaunchKernelGGL((conv_x6<MT, PT, true, 0, MODE>), dim3(a.sk_grid), blk, 0, st, a);
-    else if (a.ks == 7)
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 7, MODE>), dim3(a.sk_grid), blk, 0, st, a);
-    else if (a.ks == 3)
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 3, MODE>), dim3(a.sk_grid), blk, 0, st, a);
-    else if (a.ks == 1)
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 1, MODE>), dim3(a.sk_grid), blk, 0, st, a);
-    else
-        hipLaunchKernelGGL((conv_x6<MT, PT, false, 0, MODE>), dim3(a.sk_grid), blk, 0, st, a);
-}
-
 template <int MT, int PT>
 static void launch_x6_tile(const X6Args& a, hipStream_t st) {
-    switch (x6_mode()) {
-        case 0: launch_x6_tile_m<MT, PT, 0>(a, st); break;
-        case 1: launch_x6_tile_m<MT, PT, 1>(a, st); break;
-        case 3: launch_x6_tile_m<MT, PT, 3>(a, st); break;
-        default: launch_x6_tile_m<MT, PT, 2>(a, st); break;
-    }
+    const dim3 blk(64 * x6_waves(MT, PT));
+    if (a.small != 0)
+        hipLaunchKernelGGL((conv_x6<MT, PT, true, 0>), dim3(a.sk_grid), blk, 0, st, a);
+    else if (a.ks == 7)
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 7>), dim3(a.sk_grid), blk, 0, st, a);
+    else if (a.ks == 3)
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 3>), dim3(a.sk_grid), blk, 0, st, a);
+    else if (a.ks == 1)
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 1>), dim3(a.sk_grid), blk, 0, st, a);
+    else
+        hipLaunchKernelGGL((conv_x6<MT, PT, false, 0>), dim3(a.sk_grid), blk, 0, st, a);
     const int tiles = (a.Mpad / MT) * ((a.npix + PT - 1) / PT) * a.ngroups;
     if (a.sk_grid != tiles)
         hipLaunchKernelGGL((conv_x6_fixup<MT, PT>), dim3(tiles, MT * PT / 4 / 256), dim3(256), 0, st, a);
@@ -1073,15 +718,10 @@ void launch_conv_x6(const X6Args& a, int mt, int pt, hipStream_t st) {
     else if (mt == 256 && pt == 128) launch_x6_tile<256, 128>(a, st);
     else if (mt == 128 && pt == 64) launch_x6_tile<128, 64>(a, st);
     else if (mt == 64 && pt == 128) launch_x6_tile<64, 128>(a, st);
-    else if (mt == 64 && pt == 256) launch_x6_tile<64, 256>(a, st);
     else if (mt == 64 && pt == 64) launch_x6_tile<64, 64>(a, st);
     else throw std::invalid_argument("unsupported x6 conv tile");
 }
 
-static int grid_for(size_t total) {
-    size_t b = (total + 255) / 256;
-    return (int)(b > 8192 ? 8192 : (b ? b : 1));
-}
 
 void launch_to_x6(const float* in, int cstride, int coff, int C, int N, int HW, uint8_t* out, int cg, int goff,
                   uint32_t ps, hipStream_t st) {
@@ -1191,7 +831,7 @@ void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const fl
 //    4 waves, each 64 channels x 32 GEMM columns (one pooled row of 8 pixels x their 4
 //    quadrants): every A fragment read serves two column blocks (8 waves of 16 columns read
 //    245 KB of LDS per chunk and CU, more than the MFMAs take at 128 B/clk); the six piece
-//    products in conv_x6's MODE 2 order: bit-identical to the conv_x6 pooled launch;
+//    products in conv_x6's order: bit-identical to the conv_x6 pooled launch;
 //  * the fragments of chunk c + 1 are read during chunk c's MFMAs (two register sets); the second
 //    block's window is DMA'd over the first block's buffer behind chunk 8's MFMAs;
 //  * 70 KB of LDS: two workgroups per CU cover each other's DMA waits, barriers and epilogues.
@@ -1382,250 +1022,6 @@ void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int
     const int tiles = N * ((H + V_TH - 1) / V_TH) * ((W + V_TW - 1) / V_TW);
     hipLaunchKernelGGL(conv3_pool_win_x6_kernel, dim3(tiles), dim3(64 * V_NW), 0, st, in, ips, N, H, W, wt, bias, out,
                        ops);
-}
-
-// ---------------------------------------------------------------- conv1_1 + conv1_2 (+ pool), windowed
-// conv3_pool_win_x6 with its window computed instead of loaded: per channel block, conv1_1
-// (src/model.py:35 / :145, 3 -> 64 channels) for the 10 x 18 window around the tile straight from
-// a 3 x 12 x 20 patch of the fp32 input in LDS -- 27 fp32 FMAs per output in conv_first_x6's order,
-// bias, ReLU, split into the X6 pieces -- so conv1_1's 64-channel full-resolution tensor (741 MB
-// written and read back per bench step) never exists.  Everything after the window is
-// conv3_pool_win_x6's: bit-identical to conv_first_x6 + the pooled conv1_2.  Block 1's window is
-// built while chunk 8's MFMAs run.  78 KB of LDS: conv1_1's weights are staged per channel block.
-// Opt-in (OPOSE_CONV12_FUSED=1): it ties with the two launches it replaces -- 0.86 vs 0.17 + 0.66
-// ms serial, 1.32 vs 0.34 + 0.93 ms beside the previous step's post kernels (scripts/conv12_ab.sh).
-// The window math (1.4x the conv1_1 outputs, halo included, plus the splits) costs as much VALU
-// time as the 741 MB store and re-read it saves; the two workgroups of a CU run their window
-// phases at the same time rather than under each other's MFMAs.
-namespace {
-constexpr int V_PR = V_TH + 4, V_PC = V_TW + 4;    // input patch 12 x 20
-constexpr int V_PATCH = 3 * V_PR * V_PC;           // 720 floats
-struct Win12Smem {
-    uint4 win[V_WIN];
-    uint4 a[2][12 * 64];
-    float w11[27 * 32];  // conv1_1 weights of one channel block: [k][32]
-    float b11[64], b12[64];
-    float patch[V_PATCH];
-};
-}  // namespace
-
-__global__ __launch_bounds__(256, 2) void conv12_pool_win_x6_kernel(const float* __restrict__ x, int N, int H, int W,
-                                                                    const float* __restrict__ w11, int mpad11,
-                                                                    const float* __restrict__ b11,
-                                                                    const uint8_t* __restrict__ wt,
-                                                                    const float* __restrict__ b12,
-                                                                    uint8_t* __restrict__ out, uint32_t ops) {
-    __shared__ Win12Smem sm;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ntx = (W + V_TW - 1) / V_TW, nty = (H + V_TH - 1) / V_TH;
-    int n, y0, x0;
-    {
-        const int Gw = gridDim.x, b = blockIdx.x;
-        const int q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
-        const int t = xcd * q + min(xcd, rr) + (b >> 3);  // XCD-contiguous tiles (guide T1)
-        const int tx = t % ntx, rest = t / ntx;
-        x0 = tx * V_TW;
-        y0 = (rest % nty) * V_TH;
-        n = rest / nty;
-    }
-    const size_t HW = (size_t)H * W;
-    auto dma_a = [&](int c, int st) __attribute__((always_inline)) {
-        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(wt + (size_t)c * 12 * 64 * 16), (short)0, (int)0x7fffffff, 0x00020000);
-#pragma unroll
-        for (int row = wave; row < 12; row += V_NW)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sm.a[st] + row * 64), 16,
-                                                     (uint32_t)lane * 16u, row * 64 * 16, 0, 0);
-    };
-    auto load_w11 = [&](int cb) __attribute__((always_inline)) {
-        for (int i = tid; i < 27 * 32; i += 64 * V_NW) sm.w11[i] = w11[(size_t)(i >> 5) * mpad11 + cb * 32 + (i & 31)];
-    };
-    // conv1_1 window of channel block cb: item = (window pixel, group), consecutive threads along
-    // the row; pixels outside the frame are conv1_2's zero padding
-    auto build_window = [&](int cb) __attribute__((always_inline)) {
-        for (int it = tid; it < V_WR * V_WC * 4; it += 64 * V_NW) {
-            const int p = it % (V_WR * V_WC), gl = it / (V_WR * V_WC);
-            const int wr = p / V_WC, wc = p - wr * V_WC;
-            const int iy = y0 - 1 + wr, ix = x0 - 1 + wc;
-            float v[8];
-            if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {
-                float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int k = 0; k < 27; ++k) {
-                    const float in = sm.patch[((k / 9) * V_PR + wr + (k % 9) / 3) * V_PC + wc + k % 3];
-                    const float4 w0 = *reinterpret_cast<const float4*>(sm.w11 + k * 32 + gl * 8);
-                    const float4 w1 = *reinterpret_cast<const float4*>(sm.w11 + k * 32 + gl * 8 + 4);
-                    acc[0] = __builtin_fmaf(in, w0.x, acc[0]);
-                    acc[1] = __builtin_fmaf(in, w0.y, acc[1]);
-                    acc[2] = __builtin_fmaf(in, w0.z, acc[2]);
-                    acc[3] = __builtin_fmaf(in, w0.w, acc[3]);
-                    acc[4] = __builtin_fmaf(in, w1.x, acc[4]);
-                    acc[5] = __builtin_fmaf(in, w1.y, acc[5]);
-                    acc[6] = __builtin_fmaf(in, w1.z, acc[6]);
-                    acc[7] = __builtin_fmaf(in, w1.w, acc[7]);
-                }
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = fmaxf(acc[j] + sm.b11[cb * 32 + gl * 8 + j], 0.f);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = 0.f;
-            }
-            uint32_t hp[3][8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) split3(v[j], hp[0][j], hp[1][j], hp[2][j]);
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) {
-                uint4 w4;
-                w4.x = hp[pc][0] | (hp[pc][1] << 16);
-                w4.y = hp[pc][2] | (hp[pc][3] << 16);
-                w4.z = hp[pc][4] | (hp[pc][5] << 16);
-                w4.w = hp[pc][6] | (hp[pc][7] << 16);
-                sm.win[pc * V_PP + gl * V_GP + wr * V_RP + wc] = w4;
-            }
-        }
-    };
-    dma_a(0, 0);
-    dma_a(1, 1);
-    for (int i = tid; i < V_PATCH; i += 64 * V_NW) {
-        const int c = i / (V_PR * V_PC), r = (i / V_PC) % V_PR, cc = i % V_PC;
-        const int iy = y0 - 2 + r, ix = x0 - 2 + cc;
-        const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-        sm.patch[i] = ok ? x[((size_t)n * 3 + c) * HW + (size_t)iy * W + ix] : 0.f;
-    }
-    load_w11(0);
-    if (tid < 64) {
-        sm.b11[tid] = b11[tid];
-        sm.b12[tid] = b12[tid];
-    }
-    __syncthreads();
-    build_window(0);
-    __syncthreads();  // window 0 complete; conv1_1's block-0 weights free
-    load_w11(1);      // read at chunk 8, after several barriers
-    // this wave's 32 GEMM columns = pooled row `wave`, pooled cols 4 nb + (q >> 2) for column
-    // blocks nb = 0, 1, quad-major; lane column q = lane & 15, k-group gi = lane >> 4
-    const int q = lane & 15, gi = lane >> 4;
-    const int d = q & 3;
-    const int ty = 2 * wave + (d >> 1);
-    constexpr int PA[6] = {0, 0, 0, 1, 2, 1};
-    constexpr int PB[6] = {2, 0, 1, 0, 0, 1};
-    f32x4 acc[2][4];
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) acc[nb][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    i32x4 fb[2][2][3], fa[2][4][3];
-    auto read_frags = [&](int c, int set) __attribute__((always_inline)) {
-        const int tap = c % 9;
-        const int dy = tap / 3, dx = tap - dy * 3;
-        const uint32_t aw = (uint32_t)(uintptr_t)(lds_ptr_t)(sm.a[c & 1] + gi * 64 + q);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-            const int tx = 2 * (4 * nb + (q >> 2)) + (d & 1);
-            const uint32_t bw = (uint32_t)(uintptr_t)(lds_ptr_t)(sm.win + gi * V_GP + (ty + dy) * V_RP + (tx + dx));
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc)
-                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[set][nb][pc]) : "v"(bw), "i"(pc * V_PP * 16));
-        }
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc)
-                asm volatile("ds_read_b128 %0, %1 offset:%2"
-                             : "=v"(fa[set][mb][pc])
-                             : "v"(aw), "i"((pc * 4 * 64 + mb * 16) * 16));
-    };
-    auto fence_set = [&](int set) __attribute__((always_inline)) {
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) asm volatile("" : "+v"(fb[set][nb][pc]));
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-            for (int pc = 0; pc < 3; ++pc) asm volatile("" : "+v"(fa[set][mb][pc]));
-    };
-    auto mfma_chunk = [&](int set) __attribute__((always_inline)) {
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int tt = 0; tt < 6; ++tt)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                for (int mb = 0; mb < 4; ++mb)
-                    acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        __builtin_bit_cast(bf16x8, fa[set][mb][PA[tt]]), __builtin_bit_cast(bf16x8, fb[set][nb][PB[tt]]),
-                        acc[nb][mb], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight chunks 0 and 1
-    __syncthreads();
-    read_frags(0, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    fence_set(0);
-    auto step = [&](int c) __attribute__((always_inline)) {  // chunk c != 8
-        const int set = c & 1;
-        if (c + 1 < 18) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight chunk c + 1 (issued at c - 1)
-            __syncthreads();  // ... landed everywhere; every wave is past chunk c's reads
-            if (c + 2 < 18) dma_a(c + 2, c & 1);
-            read_frags(c + 1, set ^ 1);
-        }
-        mfma_chunk(set);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        fence_set(set ^ 1);
-    };
-    // (three loops, so that the window build stays out of the unrolled chunk loops: the register
-    // sets are indexed by the unrolled chunk number)
-#pragma unroll
-    for (int c = 0; c < 8; ++c) step(c);
-    {
-        // every wave is past chunk 7 (chunk 8's fragments in registers, set 0): block 1's window
-        // is built over block 0's while chunk 8's MFMAs run; weight chunk 10 into chunk 8's stage
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight chunk 9 (issued at chunk 7)
-        __syncthreads();
-        dma_a(10, 0);
-        mfma_chunk(0);
-        build_window(1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        read_frags(9, 1);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        fence_set(1);
-    }
-#pragma unroll
-    for (int c = 9; c < 18; ++c) step(c);
-    const int Wo = W >> 1, Ho = H >> 1;
-    const size_t HWo = (size_t)Ho * Wo;
-    const int py = (y0 >> 1) + wave;
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-        const int px = (x0 >> 1) + 4 * nb + (q >> 2);
-        const bool lead = (lane & 3) == 0 && px < Wo && py < Ho;
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) {
-            const int m = mb * 16 + 4 * gi;
-            float v[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                float mx = acc[nb][mb][j];
-                mx = fmaxf(mx, __shfl_xor(mx, 1));
-                mx = fmaxf(mx, __shfl_xor(mx, 2));
-                v[j] = fmaxf(mx + sm.b12[m + j], 0.f);
-            }
-            if (lead)
-                store4_x6(out + (((size_t)n * 8 + (m >> 3)) * HWo + (size_t)py * Wo + px) * 16 + ((m >> 2) & 1) * 8,
-                          ops, v);
-        }
-    }
-}
-
-void launch_conv12_pool_win_x6(const float* x, int N, int H, int W, const float* w11, int mpad11, const float* b11,
-                               const uint8_t* w12, const float* b12, uint8_t* out, uint32_t ops, hipStream_t st) {
-    if (H < 2 || W < 2 || mpad11 < 64) throw std::invalid_argument("conv12_pool_win_x6: shape out of range");
-    const int tiles = N * ((H + V_TH - 1) / V_TH) * ((W + V_TW - 1) / V_TW);
-    hipLaunchKernelGGL(conv12_pool_win_x6_kernel, dim3(tiles), dim3(64 * V_NW), 0, st, x, N, H, W, w11, mpad11, b11,
-                       w12, b12, out, ops);
 }
 
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <initializer_list>
 #include <map>
 #include <memory>
 #include <string>
@@ -136,8 +137,12 @@ struct DevConv {
     uint8_t* wx6 = nullptr;
     int nK6 = 0, cin_g = 0;
     bool small6 = false;
+    // 7x7 layers: the same weights in pair order for conv_win_x6 (conv_win.hip)
+    uint8_t* wx6p = nullptr;
+    int nK6p = 0;
     ~DevConv() {
         if (wx6) (void)hipFree(wx6);
+        if (wx6p) (void)hipFree(wx6p);
         if (wt) (void)hipFree(wt);
         if (bias) (void)hipFree(bias);
         if (ktab) (void)hipFree(ktab);
@@ -170,13 +175,6 @@ struct opose_ctx {
     // replay it (one launch instead of ~150: single-frame latency is launch bound)
     std::map<std::string, GraphEntry> graphs;
     bool use_graphs = getenv("OPOSE_NO_GRAPH") == nullptr;
-    // conv_window_f32 for eligible 3x3 / 7x7 layers, opt-in (OPOSE_CONV_WINDOW=1): it cuts the
-    // activation DMA 25x but measured 1-3 % slower than the im2col kernel at batch 32 -- the
-    // kernel is MFMA/clock bound (85 % MFMA busy at ~1.8-2.0 GHz under load), not load bound
-    bool conv_window = [] {
-        const char* e = getenv("OPOSE_CONV_WINDOW");
-        return e && e[0] == '1';
-    }();
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
@@ -203,12 +201,11 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_FIRST_DIRECT");
         return !(e && e[0] == '0');
     }();
-    // conv1_1 + conv1_2 + pool in one launch (conv12_pool_win_x6; needs first_direct and
-    // fused_pool), opt-in (OPOSE_CONV12_FUSED=1): bit-identical, and a tie with conv_first_x6 +
-    // conv3_pool_win_x6 (conv_x6.hip)
-    bool fused12 = [] {
-        const char* e = getenv("OPOSE_CONV12_FUSED");
-        return e && e[0] == '1';
+    // the batched 7x7 CPM convs by conv_win_x6 (input window in LDS; OPOSE_CONV7_WIN=0: conv_x6
+    // over the im2col stream, the cross-check of tests/test_gpu_x6.py)
+    bool win7 = [] {
+        const char* e = getenv("OPOSE_CONV7_WIN");
+        return !(e && e[0] == '0');
     }();
     // conv1_2 + pool by conv3_pool_win_x6 (input window in LDS; OPOSE_CONV12_WIN=0: conv_x6's
     // pooled 64 x 128 tile over the im2col stream)
@@ -216,20 +213,12 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_CONV12_WIN");
         return !(e && e[0] == '0');
     }();
-    // single-scale Body: the heat-map resize fused into the NMS tiles (gauss_nms_resize, post.hip),
-    // opt-in (OPOSE_FUSE_HEAT=1): bit-identical, but 1.10 ms per bench step against 0.47 + 0.43 ms
-    // for heat_full_f32 + gauss_nms_wide (the tiles' halos redo 2.3x the resize arithmetic, and
-    // gfx950 issues float32 VALU at the float64 rate)
-    bool fuse_heat = [] {
-        const char* e = getenv("OPOSE_FUSE_HEAT");
-        return e && e[0] == '1';
-    }();
     DevBuf frames, mids[2][kMaxScales], avg, cnt, list, peak_pos, part_cnt, score, conn, conn_cnt, records, maps_in,
         hlab, hsums, hpeaks, hfound, list_score, hsel;
     // network workspace, one set per concurrently running scale (slot s runs on scale_stream(s);
     // slot 0 is the handle's stream): input, activations, stream-K slabs
     struct NetWS {
-        DevBuf x, x6in, x6A, x6B, x6S0, x6S1, x6T0, x6T1, x6U, bufA, bufB, S0, S1, T0, T1, U, partial, skcnt;
+        DevBuf x, x6in, x6A, x6B, x6S0, x6S1, x6T0, x6T1, x6U, bufA, bufB, S0, S1, T0, T1, U, partial;
     };
     NetWS ws[kMaxScales];
     int slot = 0;
@@ -243,7 +232,7 @@ struct opose_ctx {
     hipStream_t sstream[kMaxScales] = {};
     hipEvent_t ev_fork = nullptr, ev_join[kMaxScales] = {};
     // Cross-call pipelining of opose_body_infer calls flagged OPOSE_PIPELINE (device input and
-    // output; OPOSE_PIPELINE=0 in the environment at handle creation: never).  Call k's network part (preprocess, conv stack,
+    // output).  Call k's network part (preprocess, conv stack,
     // x8 upsample) runs on `nstream`, its post-network part on `stream` after an event; call
     // k+1's network then overlaps call k's post-network kernels (latency-bound launches of a few
     // dozen workgroups, and the CUs a 236-tile conv grid leaves idle).  The x8 maps (the only
@@ -251,35 +240,15 @@ struct opose_ctx {
     // of the call two back before overwriting a set, and for `stream` whenever another entry
     // point used the shared network workspace there since (main_dirty).  Every call ends with
     // `stream` ordered after its own network part.
-    bool pipeline = [] {
-        const char* e = getenv("OPOSE_PIPELINE");
-        return !(e && e[0] == '0');
-    }();
     hipStream_t nstream = nullptr;
     hipEvent_t ev_net = nullptr, ev_main = nullptr, ev_post[2] = {nullptr, nullptr};
     // opose_wait_stream / opose_signal_stream / opose_set_stream: ordering against streams the
-    // caller owns (a framework's current stream); ev_ext is still to be waited on by `nstream`
-    // when that stream is created later
+    // caller owns (a framework's current stream)
     hipEvent_t ev_ext = nullptr, ev_sig = nullptr;
-    bool ext_for_nstream = false;
     bool post_pending[2] = {false, false};
     bool main_dirty = false;
     int mid_set = 0, next_set = 0;
     DevBuf& mid(int s) { return mids[mid_set][s]; }
-    // stream-K: split tiles reduced by the conv_sk_fixup launch (default) or in-kernel by the
-    // last arriving workgroup (OPOSE_SK_INKERNEL=1; measured 0.4 % slower at batch 32: the
-    // reducing workgroup's serial slab reads stall its next tile more than the launch costs)
-    bool sk_fixup_kernel = getenv("OPOSE_SK_INKERNEL") == nullptr;
-    // per-tile arrival counters for a stream-K launch; zero between launches (the reducing
-    // workgroup resets its tile), zero-filled whenever the buffer grows
-    int* sk_counters(int tiles) {
-        if (sk_fixup_kernel) return nullptr;
-        DevBuf& sk = w().skcnt;
-        const size_t before = sk.bytes;
-        int* c = sk.ensure<int>((size_t)tiles, stream);
-        if (sk.bytes != before) OPOSE_HIP_CHECK(hipMemsetAsync(c, 0, sk.bytes, stream));
-        return c;
-    }
     // profiling
     bool prof = false;
     bool detail = false;  // per-layer aggregation (opose_profile_enable(h, 2))
@@ -373,44 +342,30 @@ struct TileChoice {
 // SIMD) runs at ~60 %.  Stream-K (grid = all resident slots) balances the chip exactly and
 // pays for the partial slabs of tiles it splits plus one fixup launch.
 TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false, bool dp_only = false) {
-    static const int cfg[7][3] = {{128, 128, 2}, {128, 256, 1}, {256, 128, 1}, {128, 64, 3},
-                                  {64, 128, 3},  {64, 64, 4},   {64, 256, 0}};  // mt, pt, WG/CU
+    static const int cfg[6][3] = {{128, 128, 2}, {128, 256, 1}, {256, 128, 1},
+                                  {128, 64, 3},  {64, 128, 3},  {64, 64, 4}};  // mt, pt, WG/CU
     // split-bf16 kernel: 2.5x the MFMA rate per chunk, more LDS per workgroup
-    static const int occ6[7] = {1, 1, 1, 2, 2, 3, 1};
+    static const int occ6[6] = {1, 1, 1, 2, 2, 3};
     // (256x128 measured 0-2.5 % faster than 128x256 where both fit: half the im2col DMA per MFMA;
-    // 64x256 = four 64x64 waves for the M = 64 layers, opt-in (OPOSE_X6_T64X256=1): conv1_2
-    // measured 91 vs 109 TF/s with 64x128 -- an M = 64 tile loads the same im2col bytes per MFMA
-    // whatever its width, and one workgroup per CU leaves one wave per SIMD (scripts/t64_ab.sh)
-    static const double ovh6_big[7] = {1.5, 1.0, 0.96, 1.1, 1.1, 1.2, 1.0};
+    // a 64x256 tile (four 64x64 waves) for the M = 64 layers measured 91 vs 109 TF/s with 64x128
+    // on conv1_2 -- an M = 64 tile loads the same im2col bytes per MFMA whatever its width -- and
+    // was deleted)
+    static const double ovh6_big[6] = {1.5, 1.0, 0.96, 1.1, 1.1, 1.2};
     // layers of one or two small frames (C2 / C3 / single-frame C5, stream-K over the whole chip):
     // 128x128 priced like the 8-wave tiles and 64x64 higher -- measured, C2 1.91 -> 1.72 ms and
     // Hand() 10.0 -> 9.9 ms, C5 and the bench unchanged; the same weights on the bench's
-    // 32-frame layers cost 6 % (scripts/c2_tile_ab.sh; OPOSE_X6_SMALL_OVH=0 disables)
-    static const double ovh6_small[7] = {1.0, 1.0, 0.96, 1.1, 1.1, 1.6, 1.0};
-    static const bool small_ovh = [] {
-        const char* e = getenv("OPOSE_X6_SMALL_OVH");
-        return !(e && e[0] == '0');
-    }();
-    const double* ovh6 = small_ovh && (long)npix * ngroups <= 16384 ? ovh6_small : ovh6_big;
-    static const bool t64x256 = [] {
-        const char* e = getenv("OPOSE_X6_T64X256");
-        return e && e[0] == '1';
-    }();
+    // 32-frame layers cost 6 % (scripts/c2_tile_ab.sh)
+    static const double ovh6_small[6] = {1.0, 1.0, 0.96, 1.1, 1.1, 1.6};
+    const double* ovh6 = (long)npix * ngroups <= 16384 ? ovh6_small : ovh6_big;
     const double rate = x6 ? 0.4 : 1.0;
-    // relative cost per MFMA of the smaller tiles (more load/issue work per MFMA); measured
-    // with scripts/conv_timing.py, overridable for A/B runs: OPOSE_TILE_OVH="1,.95,.93,1.02,1.02,1.06"
-    static double ovh[6] = {1.0, 0.95, 0.93, 1.02, 1.02, 1.06};
-    static const bool ovh_env = [] {
-        if (const char* e = getenv("OPOSE_TILE_OVH"))
-            std::sscanf(e, "%lf,%lf,%lf,%lf,%lf,%lf", &ovh[0], &ovh[1], &ovh[2], &ovh[3], &ovh[4], &ovh[5]);
-        return true;
-    }();
-    (void)ovh_env;
+    // relative cost per MFMA of the smaller tiles of the fp32 kernel (more load/issue work per
+    // MFMA), measured with scripts/conv_timing.py
+    static const double ovh[6] = {1.0, 0.95, 0.93, 1.02, 1.02, 1.06};
     TileChoice best{64, 64, 1};
     double best_cost = 1e300;
-    for (int c = 0; c < (x6 ? 7 : 6); ++c) {  // 64x256 exists for the split-bf16 kernel only
+    for (int c = 0; c < 6; ++c) {
         const int mt = cfg[c][0], pt = cfg[c][1], occ = x6 ? occ6[c] : cfg[c][2];
-        if (Mpad % mt || (c == 6 && !t64x256)) continue;
+        if (Mpad % mt) continue;
         const long tiles = (long)(Mpad / mt) * ((npix + pt - 1) / pt) * ngroups;
         const double unit = (mt / 64.0) * (pt / 64.0) * (x6 ? ovh6[c] : ovh[c]) * rate;
         // data parallel
@@ -517,6 +472,11 @@ static void upload_conv(opose_ctx* h, int net, const std::string& key, const std
         dc->small6 = dc->cin_g == 1;
         OPOSE_HIP_CHECK(hipMalloc(&dc->wx6, wx.size() * 2));
         OPOSE_HIP_CHECK(hipMemcpy(dc->wx6, wx.data(), wx.size() * 2, hipMemcpyHostToDevice));
+        if (s0.ks == 7 && dc->Mpad % 128 == 0) {
+            x6_pack_weights_pairs(wp.data(), cout, cin_phys, s0.ks, dc->Mpad, &dc->nK6p, wx);
+            OPOSE_HIP_CHECK(hipMalloc(&dc->wx6p, wx.size() * 2));
+            OPOSE_HIP_CHECK(hipMemcpy(dc->wx6p, wx.data(), wx.size() * 2, hipMemcpyHostToDevice));
+        }
     }
     OPOSE_HIP_CHECK(hipMalloc(&dc->wt, wt.size() * 4));
     OPOSE_HIP_CHECK(hipMalloc(&dc->bias, bias.size() * 4));
@@ -576,7 +536,6 @@ static void run_conv(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W
     a.ngroups = ng;
     a.sk_grid = t.grid;
     a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
-    a.sk_cnt = h->sk_counters((a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * ng);
     double flops = 0;
     for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)a.K * a.npix;
     ProfEntry pe;
@@ -584,7 +543,7 @@ static void run_conv(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W
     if (h->detail)
         pe.detail = "layer/" + c0->name + "/" + std::to_string(t.mt) + "x" + std::to_string(t.pt) + "s" +
                     std::to_string(t.grid) + "/n" + std::to_string(a.npix);
-    if (!(h->conv_window && launch_conv_window(a, t.mt, t.pt, h->stream))) launch_conv(a, c0->ktab, t.mt, t.pt, h->stream);
+    launch_conv(a, c0->ktab, t.mt, t.pt, h->stream);
     h->prof_end(pe);
 }
 
@@ -627,15 +586,48 @@ static void run_trunk(opose_ctx* h, int net, const float* x, int N, int H, int W
 // ---------------------------------------------------------------- split-bf16 network path
 struct XAct {  // a group slice of an X6 buffer (or, f32: a channel slice of an fp32 NCHW buffer)
     void* p = nullptr;
-    int c = 0, off = 0;  // X6: groups per frame / first group; f32: channels / first channel
+    int c = 0, off = 0;  // f32: channels per frame / first channel
     uint32_t ps = 0;     // X6 piece stride (bytes)
+    X6Layout l{};        // X6 unit addressing (common.h)
     bool f32 = false;
+    bool padded = false;
 };
 
-static XAct x6act(uint8_t* p, int cg, int goff, size_t npix) {
-    const size_t ps = npix * (size_t)cg * 16;
+static XAct f32act(float* p, int c, int off) {
+    XAct a;
+    a.p = p;
+    a.c = c;
+    a.off = off;
+    a.f32 = true;
+    return a;
+}
+
+static uint32_t checked_ps(size_t ps) {
     if (ps * 3 >= 2147483648.0) throw std::invalid_argument("X6 activation >= 2 GiB: split the batch");
-    return XAct{p, cg, goff, (uint32_t)ps, false};
+    return (uint32_t)ps;
+}
+
+// dense X6 [N][cg][H*W], groups [goff, ...)
+static XAct x6act(uint8_t* p, int cg, int goff, int N, int H, int W) {
+    const size_t hw = (size_t)H * W;
+    XAct a;
+    a.p = p;
+    a.ps = checked_ps((size_t)N * cg * hw * 16);
+    a.l = X6Layout{(uint32_t)(cg * hw), (uint32_t)hw, (uint32_t)W, (uint32_t)(goff * hw)};
+    return a;
+}
+
+// padded X6P (common.h): units per (piece, group) plane
+static size_t x6p_plane(int N, int H, int W) { return (size_t)(N * (H + 3) + 4) * (W + 3); }
+
+static XAct x6pact(uint8_t* p, int cg, int goff, int N, int H, int W) {
+    const size_t P = (size_t)W + 3, plane = x6p_plane(N, H, W);
+    XAct a;
+    a.p = p;
+    a.ps = checked_ps((size_t)cg * plane * 16);
+    a.l = X6Layout{(uint32_t)((H + 3) * P), (uint32_t)plane, (uint32_t)P, (uint32_t)(goff * plane + 3 * P + 3)};
+    a.padded = true;
+    return a;
 }
 
 // pool: MaxPool2d(2, 2) (src/model.py:10-13, floor mode) fused into the epilogue; out0 is then the
@@ -663,12 +655,12 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
         X6Group& G = a.g[g];
         G.in = static_cast<const uint8_t*>(ins[g].p);
         G.in_ps = ins[g].ps;
-        G.in_cg = ins[g].c;
-        G.in_goff = ins[g].off;
+        G.in_l = ins[g].l;
         G.wt = cs[g]->wx6;
         G.bias = cs[g]->bias;
         G.out = outs[g].p;
         G.out_ps = outs[g].ps;
+        G.out_l = outs[g].l;
         G.out_c = outs[g].c;
         G.out_off = outs[g].off;
         G.out_f32 = outs[g].f32 ? 1 : 0;
@@ -679,10 +671,28 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
     if (dup.p) {
         a.g[0].out2 = dup.p;
         a.g[0].out2_ps = dup.ps;
-        a.g[0].out2_c = dup.c;
-        a.g[0].out2_off = dup.off;
+        a.g[0].out2_l = dup.l;
     }
     if (ng == 1) a.g[1] = a.g[0];
+    // batched 7x7 layers on padded inputs: the LDS-window kernel over whole 128 x 256 tiles
+    // (>= 192 of them: a data-parallel grid that fills most of the chip)
+    const long win_tiles = (long)(a.Mpad / 128) * ((a.npix + 255) / 256) * ng;
+    if (h->win7 && c0->ks == 7 && c0->wx6p && (!c1 || c1->wx6p) && !pool && in0.padded && (!c1 || in1.padded) &&
+        win_tiles >= 192 && conv_win_fits(N, H, W)) {
+        a.ngroups = ng;
+        a.nK = c0->nK6p;
+        a.g[0].wt = c0->wx6p;
+        a.g[1].wt = (c1 ? c1 : c0)->wx6p;
+        a.sk_grid = (int)win_tiles;
+        double flops = 0;
+        for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)c0->K * a.npix;
+        ProfEntry pe;
+        h->prof_begin(pe, conv_class(c0->ks), flops, 0);
+        if (h->detail) pe.detail = "layer/" + c0->name + "/win7/s" + std::to_string(win_tiles) + "/n" + std::to_string(a.npix);
+        launch_conv_win_x6(a, h->stream);
+        h->prof_end(pe);
+        return;
+    }
     // pooled convs run whole tiles (data parallel): price only those
     TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.nK, true, pool);
     if (pool) t.grid = (a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * ng;
@@ -712,28 +722,6 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
     for (size_t i = 0; i < vgg.size(); ++i) {
         const Spec& s = vgg[i];
         DevConv* c = find_conv(h, net, s.name);
-        if (i == 0 && s.cin == 3 && s.cout == 64 && s.ks == 3 && s.pad == 1 && vgg.size() > 2 && h->first_direct &&
-            h->fused12 && h->fused_pool && vgg[1].name == "conv1_2" && H % 8 == 0 && W % 2 == 0) {
-            DevConv* c2 = find_conv(h, net, vgg[1].name);
-            if (c2->cin == 64 && c2->cout == 64 && c2->ks == 3 && c2->pad == 1 && c2->Mpad == 64 && c2->nK6 == 18 &&
-                !c2->small6 && c->Mpad >= 64) {
-                // conv1_1 -> conv1_2 -> MaxPool2d in one launch: the 64-channel full-resolution
-                // tensor between them never reaches HBM
-                const size_t npo = (size_t)N * (H / 2) * (W / 2);
-                ProfEntry pe;
-                h->prof_begin(pe, "conv3x3", 2.0 * 64 * (27 + 576) * (double)npix, 0);
-                if (h->detail) pe.detail = "layer/conv1_1+conv1_2+pool/fused/n" + std::to_string(npix);
-                launch_conv12_pool_win_x6(x, N, H, W, c->wt, c->Mpad, c->bias, c2->wx6, c2->bias, A,
-                                      (uint32_t)(npo * 8 * 16), h->stream);
-                h->prof_end(pe);
-                cur = A;
-                cg = 8;
-                hh = H / 2;
-                ww = W / 2;
-                ++i;  // conv1_2 (and its pool) done
-                continue;
-            }
-        }
         if (i == 0 && s.cin == 3 && s.cout == 64 && s.ks == 3 && s.pad == 1 && vgg.size() > 1 && h->first_direct) {
             // conv1_1 straight from the fp32 input (conv_first_x6), no input split
             ProfEntry pe;
@@ -775,17 +763,16 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
             continue;
         }
         if (pooled && h->fused_pool) {  // conv + MaxPool2d(2, 2) in one launch
-            run_conv_x6(h, c, nullptr, N, hh, ww, x6act(cur, cg, 0, np),
-                        x6act(dst, og, 0, (size_t)N * (hh / 2) * (ww / 2)), XAct{}, XAct{}, true, false, XAct{},
-                        true);
+            run_conv_x6(h, c, nullptr, N, hh, ww, x6act(cur, cg, 0, N, hh, ww), x6act(dst, og, 0, N, hh / 2, ww / 2),
+                        XAct{}, XAct{}, true, false, XAct{}, true);
             cur = dst;
             cg = og;
             hh /= 2;
             ww /= 2;
             continue;
         }
-        XAct out = final_layer ? last : x6act(dst, og, 0, np);
-        run_conv_x6(h, c, nullptr, N, hh, ww, x6act(cur, cg, 0, np), out, XAct{}, XAct{}, true, false,
+        XAct out = final_layer ? last : x6act(dst, og, 0, N, hh, ww);
+        run_conv_x6(h, c, nullptr, N, hh, ww, x6act(cur, cg, 0, N, hh, ww), out, XAct{}, XAct{}, true, false,
                     final_layer ? dup : XAct{});
         cur = dst;
         cg = og;
@@ -803,20 +790,37 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
     }
 }
 
+// zero the padding units of the X6P stage buffers (two sets of two buffers): the convs never write
+// them, but a forward of another geometry on the same workspace may have put pixels there.
+// Launched every forward (inside captured graphs too): ~10 us per 32-frame bench step.
+static void clear_x6p_pads(opose_ctx* h, std::initializer_list<uint8_t*> s, int sg, std::initializer_list<uint8_t*> t,
+                           int tg, int N, int H, int W) {
+    ProfEntry pe;
+    h->prof_begin(pe, "x6p_pads", 0, 0);
+    for (uint8_t* p : s) launch_x6p_clear_pads(p, 3 * sg, N, H, W, h->stream);
+    for (uint8_t* p : t) launch_x6p_clear_pads(p, 3 * tg, N, H, W, h->stream);
+    h->prof_end(pe);
+}
+
 // bodypose_model.forward on X6 activations; output fp32 in S0 with the fp32 path's layout
 // (channel stride 185: paf [0,38), heat [38,57))
 static float* body_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
     const int hl = Hp / 8, wl = Wp / 8;
     const size_t px = (size_t)N * hl * wl;
     const int SG = 24, TG = 32, UG = 128;  // [L1 | L2 | trunk] = 5 + 3 + 16 groups; 256 / 1024 channels
-    uint8_t* S[2] = {h->w().x6S0.ensure<uint8_t>(px * SG * 48, h->stream), h->w().x6S1.ensure<uint8_t>(px * SG * 48, h->stream)};
-    uint8_t* T[2] = {h->w().x6T0.ensure<uint8_t>(px * TG * 48, h->stream), h->w().x6T1.ensure<uint8_t>(px * TG * 48, h->stream)};
+    // S (stage inputs) and T (branch activations): padded X6P, read by the 7x7 / 3x3 convs
+    const size_t plane = x6p_plane(N, hl, wl);
+    uint8_t* S[2] = {h->w().x6S0.ensure<uint8_t>(plane * SG * 48, h->stream),
+                     h->w().x6S1.ensure<uint8_t>(plane * SG * 48, h->stream)};
+    uint8_t* T[2] = {h->w().x6T0.ensure<uint8_t>(plane * TG * 48, h->stream),
+                     h->w().x6T1.ensure<uint8_t>(plane * TG * 48, h->stream)};
     uint8_t* U = h->w().x6U.ensure<uint8_t>(px * UG * 48, h->stream);
     float* O = h->w().S0.ensure<float>(px * 185, h->stream);
+    clear_x6p_pads(h, {S[0], S[1]}, SG, {T[0], T[1]}, TG, N, hl, wl);
     const int net = OPOSE_NET_BODY;
-    auto s_ = [&](int i, int goff) { return x6act(S[i], SG, goff, px); };
-    auto t_ = [&](int i, int goff) { return x6act(T[i], TG, goff, px); };
-    auto u_ = [&](int goff) { return x6act(U, UG, goff, px); };
+    auto s_ = [&](int i, int goff) { return x6pact(S[i], SG, goff, N, hl, wl); };
+    auto t_ = [&](int i, int goff) { return x6pact(T[i], TG, goff, N, hl, wl); };
+    auto u_ = [&](int goff) { return x6act(U, UG, goff, N, hl, wl); };
     run_trunk_x6(h, net, x, N, Hp, Wp, s_(0, 8), s_(1, 8));
     run_conv_x6(h, find_conv(h, net, "conv5_1_CPM_L1+L2"), nullptr, N, hl, wl, s_(0, 8), t_(0, 0), XAct{}, XAct{},
                 true, false);
@@ -840,8 +844,8 @@ static float* body_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
                         t_(t ^ 1, 0), t_(t, 16), t_(t ^ 1, 16), true, true);
             t ^= 1;
         }
-        const XAct o1 = st == 6 ? XAct{O, 185, 0, 0, true} : s_(cur ^ 1, 0);
-        const XAct o2 = st == 6 ? XAct{O, 185, 38, 0, true} : s_(cur ^ 1, 5);
+        const XAct o1 = st == 6 ? f32act(O, 185, 0) : s_(cur ^ 1, 0);
+        const XAct o2 = st == 6 ? f32act(O, 185, 38) : s_(cur ^ 1, 5);
         run_conv_x6(h, find_conv(h, net, "Mconv7" + sf + "_L1"), find_conv(h, net, "Mconv7" + sf + "_L2"), N, hl, wl,
                     t_(t, 0), o1, t_(t, 16), o2, false, st == 6);
         cur ^= 1;
@@ -854,18 +858,21 @@ static float* hand_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
     const int hl = Hp / 8, wl = Wp / 8;
     const size_t px = (size_t)N * hl * wl;
     const int SG = 19, TG = 16, UG = 64;  // [L 22 + 2 | trunk 128] = 3 + 16 groups; 128 / 512 channels
-    uint8_t* S[2] = {h->w().x6S0.ensure<uint8_t>(px * SG * 48, h->stream), h->w().x6S1.ensure<uint8_t>(px * SG * 48, h->stream)};
-    uint8_t* T[2] = {h->w().x6T0.ensure<uint8_t>(px * TG * 48, h->stream), h->w().x6T1.ensure<uint8_t>(px * TG * 48, h->stream)};
+    const size_t plane = x6p_plane(N, hl, wl);
+    uint8_t* S[2] = {h->w().x6S0.ensure<uint8_t>(plane * SG * 48, h->stream),
+                     h->w().x6S1.ensure<uint8_t>(plane * SG * 48, h->stream)};
+    uint8_t* T[2] = {h->w().x6T0.ensure<uint8_t>(plane * TG * 48, h->stream),
+                     h->w().x6T1.ensure<uint8_t>(plane * TG * 48, h->stream)};
     uint8_t* U = h->w().x6U.ensure<uint8_t>(px * UG * 48, h->stream);
     float* O = h->w().S0.ensure<float>(px * 150, h->stream);
+    clear_x6p_pads(h, {S[0], S[1]}, SG, {T[0], T[1]}, TG, N, hl, wl);
     const int net = OPOSE_NET_HAND;
-    auto s_ = [&](int i, int goff) { return x6act(S[i], SG, goff, px); };
-    auto t_ = [&](int i) { return x6act(T[i], TG, 0, px); };
+    auto s_ = [&](int i, int goff) { return x6pact(S[i], SG, goff, N, hl, wl); };
+    auto t_ = [&](int i) { return x6pact(T[i], TG, 0, N, hl, wl); };
+    const XAct u = x6act(U, UG, 0, N, hl, wl);
     run_trunk_x6(h, net, x, N, Hp, Wp, s_(0, 3), s_(1, 3));
-    run_conv_x6(h, find_conv(h, net, "conv6_1_CPM"), nullptr, N, hl, wl, s_(0, 3), x6act(U, UG, 0, px), XAct{},
-                XAct{}, true, false);
-    run_conv_x6(h, find_conv(h, net, "conv6_2_CPM"), nullptr, N, hl, wl, x6act(U, UG, 0, px), s_(1, 0), XAct{},
-                XAct{}, false, false);
+    run_conv_x6(h, find_conv(h, net, "conv6_1_CPM"), nullptr, N, hl, wl, s_(0, 3), u, XAct{}, XAct{}, true, false);
+    run_conv_x6(h, find_conv(h, net, "conv6_2_CPM"), nullptr, N, hl, wl, u, s_(1, 0), XAct{}, XAct{}, false, false);
     int cur = 1;
     for (int st = 2; st <= 6; ++st) {
         const std::string sf = "_stage" + std::to_string(st);
@@ -877,7 +884,7 @@ static float* hand_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
                         XAct{}, XAct{}, true, false);
             t ^= 1;
         }
-        const XAct o = st == 6 ? XAct{O, 150, 0, 0, true} : s_(cur ^ 1, 0);
+        const XAct o = st == 6 ? f32act(O, 150, 0) : s_(cur ^ 1, 0);
         run_conv_x6(h, find_conv(h, net, "Mconv7" + sf), nullptr, N, hl, wl, t_(t), o, XAct{}, XAct{}, false, false);
         cur ^= 1;
     }
@@ -1018,12 +1025,13 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * N * 18, h->stream));
     ProfEntry pe;
     // single scale: the float64 average equals the float32 resize output exactly -> f32 map
-    // (fuse_heat: the resize runs inside the NMS tiles, no full-resolution map at all)
     const bool f32 = ns == 1;
-    if (f32 && h->fuse_heat && gauss_nms_resize_fits(gs[0].Hs, gs[0].Ws, H, W, gs[0].up_sy)) {
-        // flops: the filter's float64 operations (2 x 37 per map pixel, bench.py GAUSS_OPS_PER_PIXEL);
-        // bytes: the x8 heat channels read
-        h->prof_begin(pe, "gauss_nms_resize", (double)N * 18 * 74.0 * H * W, (double)N * 18 * 4.0 * gs[0].Hs * gs[0].Ws);
+    if (f32 && gauss_nms_resize_fits(gs[0].Hs, gs[0].Ws, H, W, gs[0].up_sy)) {
+        // one scale, a true upsampling resize (the reference's 368-row frames at scale 0.5): the
+        // resize runs inside the NMS tiles (post.hip gauss_nms_resize) and tiles whose sources
+        // cannot produce a peak are dropped, so no full-resolution map is written or read.
+        // bytes: the x8 heat channels the tiles read (the kernel's algorithmic traffic)
+        h->prof_begin(pe, "gauss_nms_resize", 0, (double)N * 18 * 4.0 * gs[0].Hs * gs[0].Ws);
         launch_gauss_nms_resize(S.mid[0], 56, 38, 18, N, gs[0].Hs, gs[0].Ws, H, W, gs[0].up_sy, gs[0].up_sx, p.thre1,
                                 cap, cnt, list, lscore, h->stream);
         h->prof_end(pe);
@@ -1245,13 +1253,7 @@ int opose_create(int device, opose_t** out) {
     *out = nullptr;
     auto* h = new opose_ctx();
     h->device = device;
-    // OPOSE_POST_PRIORITY=1: the handle's own stream (the post-network kernels of a pipelined
-    // step) at the highest priority, for A/B runs against the default (network stream highest)
-    const char* pp = getenv("OPOSE_POST_PRIORITY");
-    int plo = 0, phi = 0;
-    const bool post_hi = pp && pp[0] == '1' && hipDeviceGetStreamPriorityRange(&plo, &phi) == hipSuccess;
-    if (hipSetDevice(device) != hipSuccess ||
-        hipStreamCreateWithPriority(&h->own_stream, hipStreamNonBlocking, post_hi ? phi : 0) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return OPOSE_E_HIP;
     }
@@ -1303,14 +1305,19 @@ int opose_wait_stream(opose_t* h, void* s) {
     OPOSE_TRY(h, {
         OPOSE_HIP_CHECK(hipSetDevice(h->device));
         const hipStream_t xs = static_cast<hipStream_t>(s);
-        if (xs == h->stream) return OPOSE_OK;
+        // Both library streams must come after `xs`: the handle's stream directly (nothing to do
+        // when `xs` is that stream), the pipelined network stream through the event even then --
+        // back-to-back pipelined calls do not otherwise order it after the handle's stream.
+        // Before the network stream exists, the first pipelined call orders it after the
+        // handle's stream (main_dirty), which by then has waited on every such `xs`.
         hipEvent_t e = lazy_event(h->ev_ext);
         OPOSE_HIP_CHECK(hipEventRecord(e, xs));
-        OPOSE_HIP_CHECK(hipStreamWaitEvent(h->stream, e, 0));
-        if (h->nstream)
-            OPOSE_HIP_CHECK(hipStreamWaitEvent(h->nstream, e, 0));
-        else
-            h->ext_for_nstream = true;
+        if (xs != h->stream) OPOSE_HIP_CHECK(hipStreamWaitEvent(h->stream, e, 0));
+        if (h->nstream) {
+            if (xs != h->nstream) OPOSE_HIP_CHECK(hipStreamWaitEvent(h->nstream, e, 0));
+        } else {
+            h->main_dirty = true;
+        }
     });
     return OPOSE_OK;
 }
@@ -1501,16 +1508,11 @@ static void pipelined_body(opose_ctx* h, int N, int H, int W, const std::vector<
         int lo = 0, hi = 0;
         OPOSE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
         // the network stream gets the higher priority: its conv grids should not wait for
-        // post-network workgroups that can run on whatever CUs are left
-        // (OPOSE_NET_PRIORITY=0: the default priority, for A/B runs)
-        const char* pe = getenv("OPOSE_NET_PRIORITY");
-        OPOSE_HIP_CHECK(hipStreamCreateWithPriority(&h->nstream, hipStreamNonBlocking, pe && pe[0] == '0' ? lo : hi));
+        // post-network workgroups that can run on whatever CUs are left (network high / post
+        // high / both default measured the same)
+        OPOSE_HIP_CHECK(hipStreamCreateWithPriority(&h->nstream, hipStreamNonBlocking, hi));
         for (hipEvent_t* e : {&h->ev_net, &h->ev_main, &h->ev_post[0], &h->ev_post[1]})
             OPOSE_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    }
-    if (h->ext_for_nstream) {  // an opose_wait_stream before this stream existed
-        OPOSE_HIP_CHECK(hipStreamWaitEvent(h->nstream, h->ev_ext, 0));
-        h->ext_for_nstream = false;
     }
     const int set = h->next_set;
     h->next_set ^= 1;
@@ -1576,7 +1578,7 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
             else
                 for (int s = 0; s < p.n_scales; ++s) scale_net(s);
         };
-        if (h->pipeline && (flags & OPOSE_PIPELINE) && (flags & OPOSE_IN_DEVICE) && (flags & OPOSE_OUT_DEVICE)) {
+        if ((flags & OPOSE_PIPELINE) && (flags & OPOSE_IN_DEVICE) && (flags & OPOSE_OUT_DEVICE)) {
             pipelined_body(h, N, H, W, gs, p, rec, net_part);
         } else if (h->scale_streams && p.n_scales > 1) {  // multi-scale pyramid (C5): scales concurrently
             enter_main(h);
@@ -2078,8 +2080,7 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
         a.ngroups = 1;
         a.sk_grid = t.grid;
         a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
-        a.sk_cnt = h->sk_counters((a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * a.ngroups);
-        if (!(h->conv_window && launch_conv_window(a, t.mt, t.pt, h->stream))) launch_conv(a, c->ktab, t.mt, t.pt, h->stream);
+        launch_conv(a, c->ktab, t.mt, t.pt, h->stream);
         OPOSE_HIP_CHECK(hipMemcpyAsync(out, yd, ny * 4, hipMemcpyDeviceToHost, h->stream));
         OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
         h->convs[0].erase("__debug__");
@@ -2112,9 +2113,9 @@ int opose_debug_conv_x6(opose_t* h, const float* x, const float* w, const float*
         a.N = N; a.H = H; a.W = W; a.ks = ks; a.pad = pad;
         a.cin_g = cg; a.small = c->small6 ? 1 : 0; a.nK = c->nK6; a.Mpad = c->Mpad; a.npix = N * HW;
         X6Group& G = a.g[0];
-        G.in = x6; G.in_ps = ips; G.in_cg = cg; G.in_goff = 0;
+        G.in = x6; G.in_ps = ips; G.in_l = x6act(x6, cg, 0, N, H, W).l;
         G.wt = c->wx6; G.bias = c->bias; G.cout = Cout; G.relu = relu; G.out2 = nullptr;
-        if (out_x6) { G.out = y6; G.out_ps = ops; G.out_c = og; G.out_off = 0; G.out_f32 = 0; }
+        if (out_x6) { G.out = y6; G.out_ps = ops; G.out_l = x6act(y6, og, 0, N, H, W).l; G.out_f32 = 0; }
         else { G.out = yd; G.out_c = Cout; G.out_off = 0; G.out_f32 = 1; }
         a.g[1] = a.g[0];
         TileChoice t = choose_tile(a.Mpad, a.npix, 1, a.nK, true);
@@ -2160,9 +2161,10 @@ int opose_debug_conv_x6_time(opose_t* h, int N, int Cin, int H, int W, int Cout,
         for (int g = 0; g < 2; ++g) {
             X6Group& G = a.g[g];
             const int gg = g < ngroups ? g : 0;
-            G.in = x6 + (size_t)gg * N * cg * HW * 16; G.in_ps = ips; G.in_cg = cg; G.in_goff = 0;
+            G.in = x6 + (size_t)gg * N * cg * HW * 16; G.in_ps = ips; G.in_l = x6act(x6, cg, 0, N, H, W).l;
             G.wt = c->wx6; G.bias = c->bias; G.cout = Cout; G.relu = 1; G.out2 = nullptr;
-            G.out = y6 + (size_t)gg * N * og * HW * 16; G.out_ps = ops; G.out_c = og; G.out_off = 0; G.out_f32 = 0;
+            G.out = y6 + (size_t)gg * N * og * HW * 16; G.out_ps = ops; G.out_l = x6act(y6, og, 0, N, H, W).l;
+            G.out_f32 = 0;
         }
         TileChoice t = choose_tile(a.Mpad, a.npix, ngroups, a.nK, true);
         if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((a.npix + pt - 1) / pt) * ngroups; }
@@ -2171,7 +2173,6 @@ int opose_debug_conv_x6_time(opose_t* h, int N, int Cin, int H, int W, int Cout,
         a.ngroups = ngroups;
         a.sk_grid = t.grid;
         a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
-        if (const char* ab = getenv("OPOSE_X6_ABLATE")) a.ablate = atoi(ab);
         launch_conv_x6(a, t.mt, t.pt, h->stream);  // warm-up
         hipEvent_t e0, e1;
         OPOSE_HIP_CHECK(hipEventCreate(&e0));
@@ -2204,9 +2205,7 @@ int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, in
         const size_t nx = (size_t)ngroups * N * Cin * H * W, ny = (size_t)ngroups * N * Cout * H * W;
         float* xd = xin.ensure<float>(nx, h->stream);
         float* yd = yout.ensure<float>(ny, h->stream);
-        // OPOSE_TIMING_RELU=1: activations with the ReLU sparsity of the real network (the chip
-        // holds a higher clock on half-zero operands than on dense noise)
-        launch_fill_hash(xd, nx, getenv("OPOSE_TIMING_RELU") ? 0x80000003u : 3u, h->stream);
+        launch_fill_hash(xd, nx, 3u, h->stream);
         ConvArgs a{};
         a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.ks = ks; a.pad = ks / 2;
         a.K = c->K; a.Kpad = c->Kpad; a.Mpad = c->Mpad; a.npix = N * H * W;
@@ -2225,16 +2224,8 @@ int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, in
         a.ngroups = ngroups;
         a.sk_grid = t.grid;
         a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
-        a.sk_cnt = h->sk_counters((a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * a.ngroups);
-        auto go = [&]() {
-            if (ablate) {
-                if (!(a.tap_major && a.ks == 7 && t.mt == 128 && t.pt == 128))
-                    throw std::invalid_argument("ablations exist for the 128x128 7x7 kernel only");
-                launch_conv_ablation(a, ablate, h->stream);
-            } else {
-                if (!(h->conv_window && launch_conv_window(a, t.mt, t.pt, h->stream))) launch_conv(a, c->ktab, t.mt, t.pt, h->stream);
-            }
-        };
+        if (ablate) throw std::invalid_argument("timing ablations were removed");
+        auto go = [&]() { launch_conv(a, c->ktab, t.mt, t.pt, h->stream); };
         go();  // warm-up
         hipEvent_t e0, e1;
         OPOSE_HIP_CHECK(hipEventCreate(&e0));

@@ -23,11 +23,7 @@ struct Conn {
 };
 
 // conv.hip
-// window variant (3x3 / 7x7, 128x256 tiles, short rows); false: not applicable, nothing launched
-size_t conv_window_lds_bytes(int mt, int pt, int ks, int W);
-bool launch_conv_window(const ConvArgs& a, int mt, int pt, hipStream_t st);
 void launch_conv(const ConvArgs& a, const int* ktab, int mt, int pt, hipStream_t st);
-void launch_conv_ablation(const ConvArgs& a, int ablate, hipStream_t st);
 void launch_fill_hash(float* p, size_t n, uint32_t seed, hipStream_t st);
 void launch_maxpool(const float* in, float* out, int NC, int H, int W, hipStream_t st);
 
@@ -40,16 +36,19 @@ void launch_from_x6(const uint8_t* in, int cg, int goff, uint32_t ps, int C, int
                     int coff, hipStream_t st);
 void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const float* wt, int Mpad, const float* bias,
                           uint8_t* out, uint32_t ops, hipStream_t st);
+// zero the padding units of `planes` X6P (piece, group) planes of an N x H x W buffer (common.h)
+void launch_x6p_clear_pads(uint8_t* buf, int planes, int N, int H, int W, hipStream_t st);
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,
                        hipStream_t st);
-// conv1_1 + conv1_2 + MaxPool2d(2, 2) fused (x fp32 [N][3][H][W] -> pooled X6 [N][8][H/2 * W/2])
 // conv1_2 (64 -> 64, 3x3 pad 1) + MaxPool2d(2, 2) from an 8-group X6 tensor, input window in LDS
 void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int W, const uint8_t* wt,
                               const float* bias, uint8_t* out, uint32_t ops, hipStream_t st);
-// conv1_1 + conv1_2 + pool, the conv1_1 window computed per channel block in LDS (no 64-channel
-// full-resolution tensor)
-void launch_conv12_pool_win_x6(const float* x, int N, int H, int W, const float* w11, int mpad11, const float* b11,
-                               const uint8_t* w12, const float* b12, uint8_t* out, uint32_t ops, hipStream_t st);
+// conv_win.hip: the 7x7 CPM convs with the im2col operand from an LDS window of the padded X6P
+// input (pair-order weights: x6_pack_weights_pairs); whole 128 x 256 tiles
+void x6_pack_weights_pairs(const float* w, int cout, int cin, int ks, int Mpad, int* nK_out,
+                           std::vector<uint16_t>& out);
+bool conv_win_fits(int N, int H, int W);
+void launch_conv_win_x6(const X6Args& a, hipStream_t st);
 // imgproc.hip
 void launch_preprocess(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int Hs,
                        int Ws, double sy, double sx, int Hp, int Wp, float pad_val, float* out, hipStream_t st);

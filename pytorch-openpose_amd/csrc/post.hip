@@ -270,7 +270,9 @@ __global__ __launch_bounds__(256) void gauss_nms_wide(const T* __restrict__ avg,
 
 // Single-scale Body path with heat_full's cubic resize (src/body.py:57) fused in: the NMS window
 // is resized from the x8 map (mid) inside the tile, so the full-resolution float32 map is neither
-// written nor re-read (8 bytes per pixel and part).  The footprint's source rows are resized
+// written nor re-read (8 bytes per pixel and part), and a tile whose sources are all too small to
+// produce a peak is dropped before any arithmetic (on the bench's maps ~60 % of the tiles: a
+// part's peaks sit in a few places of the frame).  The footprint's source rows are resized
 // horizontally once into LDS (aliasing the smoothing plane), then each vertical-pass thread
 // combines its 40 window rows from them -- cubic_resize_rows<1>'s arithmetic in its order, so the
 // window holds exactly the values launch_heat_full_f32 would have stored (0.f + v).  The score of
@@ -308,6 +310,30 @@ __global__ __launch_bounds__(256) void gauss_nms_resize(const float* __restrict_
     const int lo = s_lo, hi = s_hi;
     {
         const CubicTap tx = cubic_tap(reflect_idx(x0 - 13 + c, W), sx, Ws);
+        // Cold-tile skip, decided on the source before any arithmetic: every resized value of the
+        // footprint is sum_i ty.c[i] * sum_j tx.c[j] * q_ij over the source values q this loop
+        // reads, and the cubic (A = -0.75) weights of one axis sum to at most 1.375 in absolute
+        // value (t = 0.5), so |resized| <= 1.890625 * max|q| (float32 rounding: < 1e-6 relative;
+        // 1.9 covers it).  The smoothing is a convex combination of the resized footprint, so
+        // when 1.9 * max|q| is below the threshold no output of the tile can pass `> thre`:
+        // nothing to resize, filter or report (the exact criterion gauss_wide_tail applies to
+        // the resized values, taken earlier and more conservatively).  NaN sources count as
+        // below, as in gauss_wide_tail (a NaN only ever removes peaks).
+        float mx = 0.f;
+        for (int r0 = lo + h; r0 <= hi; r0 += 16) {
+            float q[8][4];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float* row = plane + (size_t)min(r0 + 2 * k, hi) * Ws;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) q[k][j] = row[tx.i[j]];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) mx = fmaxf(mx, fabsf(q[k][j]));
+        }
+        if (!__syncthreads_or(1.9 * (double)mx >= gauss_skip_below(thre))) return;
         for (int r0 = lo + h; r0 <= hi; r0 += 16) {  // 8 rows per round, loads issued first
             float q[8][4];
 #pragma unroll

@@ -1,0 +1,59 @@
+// x6.h — device helpers of the split-bf16 ("X6") convolution kernels (conv_x6.hip, conv_win.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+
+namespace opose {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+namespace x6 {
+
+constexpr int x6_waves(int mt, int pt) { return mt * pt >= 32768 ? 8 : 4; }
+
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+    uint32_t u = __float_as_uint(x);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return u >> 16;
+}
+
+// x -> three bf16 pieces, x0 + x1 + x2 == x exactly (each remainder is exact by Sterbenz)
+__device__ __forceinline__ void split3(float x, uint32_t& h0, uint32_t& h1, uint32_t& h2) {
+    h0 = bf16_rne(x);
+    const float r = x - __uint_as_float(h0 << 16);
+    h1 = bf16_rne(r);
+    const float r2 = r - __uint_as_float(h1 << 16);
+    h2 = bf16_rne(r2);
+}
+
+__device__ __forceinline__ float join3(uint32_t h0, uint32_t h1, uint32_t h2) {
+    return (__uint_as_float(h0 << 16) + __uint_as_float(h1 << 16)) + __uint_as_float(h2 << 16);
+}
+
+// write 4 consecutive channels (4hk .. 4hk+3 of a group) of one pixel, split, into the 3 planes
+__device__ __forceinline__ void store4_x6(uint8_t* unit, uint32_t ps, const float (&v)[4]) {
+    uint32_t h[3][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) split3(v[t], h[0][t], h[1][t], h[2][t]);
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+        uint2 w;
+        w.x = h[pc][0] | (h[pc][1] << 16);
+        w.y = h[pc][2] | (h[pc][3] << 16);
+        *reinterpret_cast<uint2*>(unit + (size_t)pc * ps) = w;
+    }
+}
+
+// unit index of (frame n, group g of the slice, y, x) in an X6 plane (common.h X6Layout)
+__device__ __forceinline__ uint32_t x6_unit(const X6Layout& l, int n, int g, int y, int x) {
+    return l.o0 + (uint32_t)n * l.fs + (uint32_t)g * l.gs + (uint32_t)y * l.rs + (uint32_t)x;
+}
+
+}  // namespace x6
+using namespace x6;
+
+}  // namespace opose

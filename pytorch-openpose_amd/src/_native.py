@@ -127,17 +127,16 @@ class Handle:
             raise OposeError(rc, "opose_create failed (no usable HIP device?)")
         self.h = h
         self.device = device
-        # The handle's main stream is a torch pool stream (torch never destroys those): tensors
-        # whose last use is queued there (Handle.hold -> record_stream) can then be freed at any
-        # time, even after this handle is gone, without the allocator touching a dead stream.
+        # The handle runs on the library's own stream until the first device-tensor call
+        # (wait_torch / signal_torch / hold): numpy-only callers never import torch or touch its
+        # HIP context.  From then on the handle's stream is a torch pool stream (torch never
+        # destroys those), so tensors whose last use is queued there (Handle.hold ->
+        # record_stream) can be freed at any time, even after this handle is gone.  Torch hands
+        # out its 32 pool streams per device round-robin: an unrelated torch.cuda.Stream() may be
+        # the same HIP stream.  That only serialises the two users; opose_wait_stream /
+        # opose_signal_stream order the library's streams correctly when a caller's stream is
+        # the handle's own (tests/test_gpu_streams.py).
         self._torch_stream_obj = None
-        try:
-            import torch
-            if torch.cuda.is_available():
-                self._torch_stream_obj = torch.cuda.Stream(device=torch.device("cuda", device))
-                self.set_stream(self._torch_stream_obj.cuda_stream)
-        except ImportError:
-            pass
 
     def close(self):
         if getattr(self, "h", None):
@@ -168,12 +167,25 @@ class Handle:
     def stream(self) -> int:
         return lib.opose_get_stream(self.h) or 0
 
+    def torch_stream(self):
+        """The handle's stream as a torch.cuda.Stream (adopting a torch pool stream first): what
+        consumers of pipelined outputs order themselves on."""
+        self._adopt_torch_stream()
+        return self._torch_stream_obj
+
     def synchronize(self):
         self.check(lib.opose_synchronize(self.h))
 
     # ---- ordering against torch's current stream (every device-tensor entry point)
+    def _adopt_torch_stream(self):
+        if self._torch_stream_obj is None:
+            import torch
+            self._torch_stream_obj = torch.cuda.Stream(device=torch.device("cuda", self.device))
+            self.set_stream(self._torch_stream_obj.cuda_stream)  # ordered after the library's own stream
+
     def _torch_stream(self):
         import torch
+        self._adopt_torch_stream()
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream or None)
 
     def wait_torch(self):
@@ -188,8 +200,9 @@ class Handle:
     def hold(self, *tensors):
         """Keep the caching allocator from reusing these tensors' memory until the handle's
         stream passes this point (asynchronous calls whose outputs stay on the handle's stream)."""
+        self._adopt_torch_stream()
         st = self._torch_stream_obj
-        if st is None or st.cuda_stream != self.stream():
+        if st.cuda_stream != self.stream():
             raise RuntimeError("Handle.hold needs the handle on its torch pool stream (set_stream changed it)")
         for t in tensors:
             t.record_stream(st)

@@ -13,12 +13,20 @@ one crop-batched Hand pass) instead of one frame at a time; per-frame results ar
 `src.pipeline.motion_data_every_frame`.  Any iterable of uint8 BGR frames works as a source;
 `VideoFrames` reads a video file through OpenCV when it is installed (it is not part of this
 image: decode elsewhere and pass the frames).
+
+Ingest (the reference's DataLoader over decoded frames, srcmx/Batch_model.py:36-52, 409-412, into
+the per-video loop of srcmx/MotionEstimation.py:61-76): with a GPU, `extract_motion_data` streams
+the batches through two pinned host buffers and two device frame buffers.  While batch k runs
+Body on the GPU (Body.infer_records, pipelined with batch k-1's post-processing), batch k+1 is
+cropped into the other pinned buffer and uploaded on its own copy stream, and batch k-1's
+records (downloaded asynchronously to pinned memory) are decoded into poses on the host, its
+hands running through Hand on the Hand handle's stream.  The poses are those of the host path
+(`device=False`: Body.batch per batch), bit for bit.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from .pipeline import motion_data_frames
 
 
 class VideoFrames(object):
@@ -56,26 +64,108 @@ def crop_roi(frame, recpoint):
     return frame[recpoint[0][1]:recpoint[1][1], recpoint[0][0]:recpoint[1][0], :]
 
 
-def extract_motion_data(frames, body, hand=None, outpath=None, recpoint=None, mode="body", batch=32):
+def _batches(frames, recpoint, batch):
+    buf = []
+    for frame in frames:
+        buf.append(crop_roi(np.asarray(frame), recpoint))
+        if len(buf) == batch:
+            yield buf
+            buf = []
+    if buf:
+        yield buf
+
+
+def _host_poses(frames, body, hand, recpoint, mode, batch):
+    from .pipeline import poses_from_results
+    out = []
+    for b in _batches(frames, recpoint, batch):
+        arr = np.stack([np.ascontiguousarray(f) for f in b])
+        out.append(poses_from_results(body.batch(arr), arr, hand, mode))
+    return out
+
+
+class _DeviceIngest(object):
+    """Two pinned host frame buffers -> two device frame buffers (one copy stream each) ->
+    Body.infer_records(pipeline=True) -> records downloaded to pinned host memory on the
+    handle's stream; at most two batches in flight."""
+
+    def __init__(self, body, batch, H, W):
+        import torch
+        self.torch = torch
+        self.body = body
+        dev = torch.device("cuda", body.handle.device)
+        rb = body.handle.record_bytes()
+        self.host = [torch.empty((batch, H, W, 3), dtype=torch.uint8).pin_memory() for _ in range(2)]
+        self.dev = [torch.empty((batch, H, W, 3), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.rdev = [torch.empty((batch, rb), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.rhost = [torch.empty((batch, rb), dtype=torch.uint8).pin_memory() for _ in range(2)]
+        self.cps = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        self.up_done = [None, None]    # upload of buffer i finished with host[i]
+        self.rec_done = [None, None]   # records of buffer i on the host
+        self.lib = body.handle.torch_stream()
+
+    def submit(self, i, frames):
+        torch = self.torch
+        n = len(frames)
+        if self.up_done[i] is not None:
+            self.up_done[i].synchronize()  # host[i] free: its previous upload completed
+        np.stack(frames, out=self.host[i][:n].numpy())
+        cp = self.cps[i]
+        cp.wait_stream(self.lib)  # the call that last read dev[i] / wrote rdev[i] is done with them
+        with torch.cuda.stream(cp):
+            self.dev[i][:n].copy_(self.host[i][:n], non_blocking=True)
+            self.up_done[i] = torch.cuda.Event()
+            self.up_done[i].record(cp)
+            # the library orders itself after this stream (opose_wait_stream): the upload above
+            self.body.infer_records(self.dev[i][:n], self.rdev[i][:n], pipeline=True)
+        with torch.cuda.stream(self.lib):
+            self.rhost[i][:n].copy_(self.rdev[i][:n], non_blocking=True)
+            self.rec_done[i] = torch.cuda.Event()
+            self.rec_done[i].record(self.lib)
+
+    def results(self, i, n):
+        self.rec_done[i].synchronize()
+        return [self.body._decode(r) for r in self.rhost[i][:n].numpy()]
+
+
+def _device_poses(frames, body, hand, recpoint, mode, batch):
+    from .pipeline import poses_from_results
+    out, ing, pending, k = [], None, None, 0
+    for b in _batches(frames, recpoint, batch):
+        if ing is None:
+            H, W = b[0].shape[:2]
+            ing = _DeviceIngest(body, batch, H, W)
+        if any(f.shape != b[0].shape for f in b) or b[0].shape[:2] != tuple(ing.host[0].shape[1:3]):
+            raise ValueError("frames must have equal sizes after cropping")
+        i = k % 2
+        ing.submit(i, b)
+        if pending is not None:  # the previous batch's poses while this one runs on the GPU
+            pi, pframes = pending
+            out.append(poses_from_results(ing.results(pi, len(pframes)), pframes, hand, mode))
+        pending = (i, b)
+        k += 1
+    if pending is not None:
+        pi, pframes = pending
+        out.append(poses_from_results(ing.results(pi, len(pframes)), pframes, hand, mode))
+    return out
+
+
+def extract_motion_data(frames, body, hand=None, outpath=None, recpoint=None, mode="body", batch=32, device=None):
     """MotionMat [n_frames, 18 | 60, 3] for an iterable of uint8 BGR frames (equal sizes after
     cropping).  mode "body" (18 joints) or "bodyhand" (needs `hand`); saved with joblib.dump
-    when `outpath` is given, like Extract_MotionData_from_Video."""
+    when `outpath` is given, like Extract_MotionData_from_Video.  device=None: the pinned,
+    double-buffered GPU ingest when torch sees a GPU, else host batches (Body.batch)."""
     if mode not in ("body", "bodyhand"):
         raise ValueError("mode must be 'body' or 'bodyhand'")
     if mode == "bodyhand" and hand is None:
         raise ValueError("'bodyhand' mode needs a Hand")
-    out, buf = [], []
-
-    def flush():
-        if buf:
-            out.append(motion_data_frames(body, hand, np.stack(buf), mode))
-            buf.clear()
-
-    for frame in frames:
-        buf.append(np.ascontiguousarray(crop_roi(np.asarray(frame), recpoint)))
-        if len(buf) == batch:
-            flush()
-    flush()
+    if device is None:
+        try:
+            import torch
+            device = torch.cuda.is_available()
+        except ImportError:
+            device = False
+    out = (_device_poses if device else _host_poses)(frames, body, hand, recpoint, mode, batch)
     joints = 60 if mode == "bodyhand" else 18
     motion = np.concatenate(out) if out else np.zeros((0, joints, 3))
     if outpath is not None:

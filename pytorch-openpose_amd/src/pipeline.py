@@ -54,8 +54,14 @@ def motion_data_frames(body, hand, frames, mode: str = "bodyhand") -> np.ndarray
     sequence for all frames, then every selected hand of every frame in one crop-batched Hand
     launch per scale (SURVEY §8 f rank 1).  Returns [T, 60, 3] ("bodyhand") or [T, 18, 3]."""
     frames = np.asarray(frames)
-    results = body.batch(frames)
-    T = len(frames)
+    return poses_from_results(body.batch(frames), frames, hand, mode)
+
+
+def poses_from_results(results, frames, hand, mode: str = "bodyhand") -> np.ndarray:
+    """The glue of `MotionData_every_frame` (srcmx/MotionEstimation.py:139-216) after Body:
+    results[t] = (candidate, subset) of frames[t] -> [T, 60, 3] ("bodyhand") or [T, 18, 3]; the
+    hands of all frames go through one crop-batched Hand call."""
+    T = len(results)
     poses = np.zeros((T, 60, 3))
     jobs = []  # (frame, crop, x0, y0, w, is_left)
     for t, (candidate, subset) in enumerate(results):

@@ -8,6 +8,8 @@ C3  Body()+Hand() per frame (src.pipeline.motion_data_every_frame, mode "bodyhan
     the selected person, 368x368-class crops, 4 hand scales) and Hand() alone on a 368x368 crop.
 C5  1920x1080 frames with scale_search [0.5, 1.0, 1.5, 2.0] (averaged heat maps), device
     resident batches -> frames/s per GPU (C5 shards frames over 8 GPUs like C4).
+f2  motion-matrix extraction (src/motion.py) over 256 decoded 368x656 frames, body and
+    bodyhand modes: the GPU ingest against host batches.
 """
 from __future__ import annotations
 
@@ -85,6 +87,22 @@ def main():
     out["C3_bodyhand_batched_8frames_ms_per_frame"] = ms / T
     out["C3_bodyhand_batched_hands_per_8frames"] = int(np.median(hands))
 
+    # f2: motion-matrix extraction over a decoded video (src/motion.py extract_motion_data:
+    # pinned double-buffered uploads, pipelined Body, poses of batch k-1 decoded while batch k
+    # runs), frames already decoded in host memory (no video decoder in this image)
+    from src.motion import extract_motion_data
+    video = rng.integers(0, 256, (256, 368, 656, 3), dtype=np.uint8)
+    for mode in ("body", "bodyhand"):
+        extract_motion_data(video[:64], body, hand, mode=mode, batch=32)  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        extract_motion_data(video, body, hand, mode=mode, batch=32)
+        torch.cuda.synchronize()
+        out[f"f2_motion_{mode}_frames_per_s"] = len(video) / (time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        extract_motion_data(video[:96], body, hand, mode=mode, batch=32, device=False)
+        out[f"f2_motion_{mode}_host_batches_frames_per_s"] = 96 / (time.perf_counter() - t0)
+
     # fast mode (srcmx/Batch_model.py Batch_body) on the C4 batch: 32 frames 368x656 per GPU
     from src.batch_model import Batch_body
     bb = Batch_body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE), peaks_per_part=256, max_people=128)
@@ -116,8 +134,8 @@ def main():
     out["C5_1080p_4scale_ms_per_batch"] = ms
     out["C5_1080p_4scale_frames_per_s_per_gpu"] = B / (ms * 1e-3)
     # the same batches back to back with OPOSE_PIPELINE (each batch's post-processing overlaps
-    # the next batch's network; the scales of a batch then run one after another on the network
-    # stream) -- the video-throughput reading of C5
+    # the next batch's network; the scales of a batch run concurrently on per-scale streams
+    # forked from and joined into the network stream) -- the video-throughput reading of C5
     recs5 = [torch.empty_like(rec5) for _ in range(2)]
     for w in range(2):
         body5.infer_records(f5, recs5[w], pipeline=True)

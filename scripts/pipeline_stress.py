@@ -34,6 +34,6 @@ for trial in range(T):
                     d = [r for r in range(rows) if not np.array_equal(s[r], es[r])]
                     print(f"  trial {trial} call {call} b{i} f{f}: subset {s.shape} vs {es.shape}, first diff row "
                           f"{d[:1]}: {s[d[0]] if d else None} vs {es[d[0]] if d else None}", flush=True)
-print(f"lib={os.environ.get('OPOSE_LIB', 'head')} small_ovh={os.environ.get('OPOSE_X6_SMALL_OVH', '1')} "
+print(f"lib={os.environ.get('OPOSE_LIB', 'head')} "
       f"shape={NB}x{HB}x{WB} scales={len(scales)}: "
       f"{frames} frames, candidate mismatches {bad_c}, subset-only mismatches {bad_s}", flush=True)

@@ -1,6 +1,6 @@
 """Times the split-bf16 conv kernel on the bench's layer shapes (32 frames of 184x328 input),
-default tile/stream-K choice; one JSON line per shape.  A/B: run under different OPOSE_X6_*
-environment settings."""
+default tile/stream-K choice; one JSON line per shape.  A/B: OPOSE_LIB=<other build> (build_alt.sh),
+AB_TILE=MTxPT, AB_SPLITS=<stream-K grids>."""
 import ctypes as C
 import json
 import os
@@ -13,7 +13,6 @@ from src import _native  # noqa: E402
 h = _native.Handle(0)
 tag = os.environ.get("AB_TAG", "")
 ms = C.c_float()
-ablations = [int(v) for v in os.environ.get("AB_ABLATE", "0").split(",")]
 layers = os.environ.get("AB_LAYERS")
 for name, N, Cin, H, W, Cout, ks, ng in [("Mconv2-5", 32, 128, 23, 41, 128, 7, 2), ("Mconv1", 32, 185, 23, 41, 256, 7, 1),
                                           ("conv1_2", 32, 64, 184, 328, 64, 3, 1),
@@ -30,11 +29,9 @@ for name, N, Cin, H, W, Cout, ks, ng in [("Mconv2-5", 32, 128, 23, 41, 128, 7, 2
         continue
     flops = 2.0 * N * H * W * Cout * Cin * ks * ks * ng
     for sp in [int(v) for v in os.environ.get("AB_SPLITS", "0").split(",")]:
-     for ab in ablations:  # OPOSE_X6_ABLATE bits (timing only, wrong results): see common.h X6Args
-        os.environ["OPOSE_X6_ABLATE"] = str(ab)
         mt, pt = (128, 256) if sp else (0, 0)
         if os.environ.get("AB_TILE"):  # e.g. AB_TILE=256x128
             mt, pt = (int(v) for v in os.environ["AB_TILE"].split("x"))
         h.check(_native.lib.opose_debug_conv_x6_time(h.h, N, Cin, H, W, Cout, ks, ng, mt, pt, sp, 20, C.byref(ms)))
-        print(json.dumps(dict(tag=tag + (f"sk{sp}" if sp else ""), layer=name, ablate=ab, ms=round(ms.value, 4),
+        print(json.dumps(dict(tag=tag + (f"sk{sp}" if sp else ""), layer=name, ms=round(ms.value, 4),
                               tf=round(flops / ms.value / 1e9, 1))), flush=True)

@@ -81,15 +81,6 @@ def test_conv_7x7_tiles(native, handle, cout, mt, pt, splits):
     _conv_case(native, handle, 3, 128, 23, 41, cout, 7, relu=True, mt=mt, pt=pt, splits=splits, seed=4)
 
 
-def test_conv_streamk_inkernel_reduction(native, monkeypatch):
-    # the opt-in in-kernel stream-K reduction (last arriving workgroup sums the parts)
-    monkeypatch.setenv("OPOSE_SK_INKERNEL", "1")
-    h = native.Handle(0)
-    for mt, pt, splits in ((128, 256, 7), (128, 128, 9), (64, 64, 13)):
-        _conv_case(native, h, 3, 128, 23, 41, 128, 7, relu=True, mt=mt, pt=pt, splits=splits, seed=6)
-    _conv_case(native, h, 2, 96, 17, 29, 256, 3, relu=False, mt=256, pt=128, splits=6, seed=5)
-
-
 @pytest.mark.parametrize("splits", [0, 1, 6])
 def test_conv_256_rows(native, handle, splits):
     _conv_case(native, handle, 2, 96, 17, 29, 256, 3, relu=False, mt=256, pt=128, splits=splits, seed=5)
@@ -278,26 +269,3 @@ def test_graph_replay_matches_eager(native):
         out = body(img)
         if ref is not None:
             assert np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1])
-
-
-@pytest.mark.parametrize("N,Cin,H,W,Cout,ks,splits", [
-    (1, 185, 23, 41, 256, 7, 0),    # Mconv1: padded channel block, two M tiles
-    (20, 64, 5, 6, 128, 7, 0),      # windows spanning many tiny frames (halo > frame)
-    (3, 128, 23, 41, 128, 7, 11),   # stream-K ranges starting mid channel block
-    (2, 256, 46, 82, 256, 3, 0),    # conv3_x rows (window 422 floats)
-    (1, 64, 9, 200, 100, 3, 3),     # wide rows, M = 100 padded to 128
-])
-def test_conv_window_kernel(native, window_handle, N, Cin, H, W, Cout, ks, splits):
-    # opt-in conv_window_f32 (flat activation window per channel block) on 128x256 tiles
-    _conv_case(native, window_handle, N, Cin, H, W, Cout, ks, relu=True, mt=128, pt=256, splits=splits, seed=7)
-    # and the default im2col kernel on the same case
-    _conv_case(native, native.Handle(0), N, Cin, H, W, Cout, ks, relu=True, mt=128, pt=256, splits=splits, seed=7)
-
-
-@pytest.fixture(scope="module")
-def window_handle(native):
-    os.environ["OPOSE_CONV_WINDOW"] = "1"
-    try:
-        return native.Handle(0)
-    finally:
-        del os.environ["OPOSE_CONV_WINDOW"]

@@ -114,3 +114,22 @@ def test_extract_motion_data_matches_per_frame(nets, tmp_path):
     assert np.array_equal(joblib.load(out), got)
     body_only = extract_motion_data(video, body, recpoint=rec, mode="body", batch=4)
     assert body_only.shape == (5, 18, 3) and np.array_equal(body_only[:, :, :2], got[:, :18, :2])
+
+
+def test_extract_motion_data_device_ingest_equals_host(nets):
+    """The pinned, double-buffered GPU ingest (device=True: uploads on copy streams, pipelined
+    Body.infer_records, records downloaded asynchronously, poses of batch k-1 decoded while batch
+    k runs) against host batches (device=False: Body.batch): identical poses, both modes, a
+    ragged last batch, and more batches than buffers."""
+    from src.motion import extract_motion_data
+    from src.weights import BENCH_OUT_SCALE, seeded_state_dict
+    _, hsd, Body, Hand = nets
+    body = Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE))
+    hand = Hand(hsd)
+    video = np.random.default_rng(62).integers(0, 256, (11, 200, 260, 3), dtype=np.uint8)
+    rec = [(4, 6), (248, 190)]
+    for mode in ("body", "bodyhand"):
+        dev = extract_motion_data(iter(video), body, hand, recpoint=rec, mode=mode, batch=3, device=True)
+        host = extract_motion_data(iter(video), body, hand, recpoint=rec, mode=mode, batch=3, device=False)
+        assert dev.shape == host.shape == (11, 60 if mode == "bodyhand" else 18, 3)
+        assert np.array_equal(dev, host), mode

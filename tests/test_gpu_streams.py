@@ -52,6 +52,71 @@ def test_infer_records_waits_for_torch_stream(body):
     _same(body.decode_records(rec), exp)
 
 
+def test_producer_on_the_handle_stream_then_pipelined(body):
+    """Frames written on the handle's own stream (a caller that orders itself on
+    handle.torch_stream(), as bench.py's gather does), then two back-to-back pipelined calls: the
+    pipelined network stream must wait for that stream too, not only for torch's other streams."""
+    frames = np.random.default_rng(12).integers(0, 256, (2, 184, 328, 3), dtype=np.uint8)
+    exp = body.batch(frames)
+    src = torch.from_numpy(frames).cuda()
+    dst = torch.zeros_like(src)
+    torch.cuda.synchronize()
+    for _ in range(2):  # network stream created; back-to-back pipelined calls (no main_dirty)
+        body.infer_records(dst, pipeline=True)
+    body.handle.synchronize()
+    with torch.cuda.stream(body.handle.torch_stream()):
+        torch.cuda._sleep(50_000_000)  # the frames land only after this spin
+        dst.zero_()
+        dst.copy_(src)
+        r1 = body.infer_records(dst, pipeline=True)
+        r2 = body.infer_records(dst, pipeline=True)
+    _same(body.decode_records(r1), exp)
+    _same(body.decode_records(r2), exp)
+
+
+def test_pipelined_multiscale_matches_serial():
+    """Pipelined two-scale batches (each batch's scales run concurrently on per-scale streams
+    forked from the network stream, its post-processing under the next batch's networks),
+    alternating inputs and record buffers, against the serial host path."""
+    from src.body import Body
+    from src.weights import BENCH_OUT_SCALE, seeded_state_dict
+    body2 = Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE), scale_search=(0.5, 1.0))
+    rng = np.random.default_rng(13)
+    batches = [rng.integers(0, 256, (2, 120, 200, 3), dtype=np.uint8) for _ in range(2)]
+    exp = [body2.batch(b) for b in batches]
+    dev = [torch.from_numpy(b).cuda() for b in batches]
+    rb = body2.handle.record_bytes()
+    recs = [torch.empty((2, rb), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+    for k in range(6):
+        body2.infer_records(dev[k % 2], recs[k % 2], pipeline=True)
+        if k % 2:
+            body2.handle.synchronize()
+            for i in range(2):
+                _same(body2.decode_records(recs[i]), exp[i])
+
+
+def test_hand_scale_streams_bit_identical():
+    """Hand(): the four scales on concurrent streams (default) and one after another
+    (OPOSE_SCALE_STREAMS=0, read when the handle is created) give identical peaks."""
+    from src.hand import Hand
+    from src.weights import seeded_state_dict
+    crop = np.random.default_rng(14).integers(0, 256, (150, 150, 3), dtype=np.uint8)
+    sd = seeded_state_dict("hand", 0)
+    a = Hand(sd)(crop)
+    old = os.environ.get("OPOSE_SCALE_STREAMS")
+    os.environ["OPOSE_SCALE_STREAMS"] = "0"
+    try:
+        serial = Hand(sd)
+    finally:
+        if old is None:
+            del os.environ["OPOSE_SCALE_STREAMS"]
+        else:
+            os.environ["OPOSE_SCALE_STREAMS"] = old
+    b = serial(crop)
+    assert a.dtype == b.dtype and np.array_equal(a, b)
+
+
 def test_forward_waits_for_half_input(body):
     x = torch.from_numpy(np.random.default_rng(6).standard_normal((1, 3, 64, 96)).astype(np.float32))
     xh = x.half()
