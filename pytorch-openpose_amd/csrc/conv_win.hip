@@ -19,6 +19,8 @@
 //    (0,2) (0,0) (0,1) | barrier | (1,0) (2,0) (1,1), fragments refilled after their last use.
 //  * Whole tiles only (data-parallel grid of >= ~200 tiles: the batched path); the host falls
 //    back to conv_x6 (stream-K) for small problems and when a window would exceed WMAX.
+//  * The same kernel runs the batched 3x3 convs on padded inputs (trunk conv3_x / conv4_x and
+//    the stage-1 CPM convs, src/model.py:41-62): a window per group serves 9 taps.
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -39,7 +41,9 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     constexpr int A_U = 12 * MT;                 // 16-byte units per weight stage
     constexpr int A_PW = A_U / 64 / NW;          // weight DMA instructions per wave per chunk
     constexpr int WBUF = 3 * WMAX;               // units per window buffer (3 pieces)
-    static_assert(A_U % (64 * NW) == 0 && A_PW == 3 && WMAX % 64 == 0 && TAPS >= 16, "conv_win_x6 tile");
+    // TAPS >= 9: a group ends at most once per chunk, and the window of group g + 2 (issued after
+    // the last chunk of group g) lands at least one barrier before its first read
+    static_assert(A_U % (64 * NW) == 0 && A_PW == 3 && WMAX % 64 == 0 && TAPS >= 9, "conv_win_x6 tile");
 
     __shared__ __attribute__((aligned(16))) uint4 lds[2 * A_U + 2 * WBUF];
     __shared__ float s_bias[MT];
@@ -364,27 +368,39 @@ void x6_pack_weights_pairs(const float* w, int cout, int cin, int ks, int Mpad, 
         }
 }
 
-constexpr int kWinMax = 768;  // window units per (piece, group): 17 padded rows of a 41-wide map
+// window capacities (units per (piece, group)): LDS = 2 weight stages (48 KB) + 2 x 3 x WMAX units
+constexpr int kWinSmall = 768, kWinLarge = 1088;
 
-// largest window (units) a tile of PT pixels needs on an N x H x W batch, 7x7
-int conv_win_units(int N, int H, int W, int pt) {
-    const int HW = H * W, P = W + 3, npix = N * HW;
+// largest window (units) a tile of PT pixels needs on an N x H x W batch for a KS x KS conv
+int conv_win_units(int N, int H, int W, int ks, int pt) {
+    const int HW = H * W, P = W + 3, npix = N * HW, pad = ks / 2;
     int worst = 0;
     for (int p0 = 0; p0 < npix; p0 += pt) {
         const int p1 = std::min(p0 + pt, npix) - 1;
         auto prow = [&](int p) { return 3 + (p / HW) * (H + 3) + (p % HW) / W; };
-        worst = std::max(worst, (prow(p1) - prow(p0) + 7) * P + 3);
+        worst = std::max(worst, (prow(p1) - prow(p0) + 2 * pad + 1) * P + pad);
     }
     return worst;
 }
 
-bool conv_win_fits(int N, int H, int W) { return conv_win_units(N, H, W, 256) <= kWinMax; }
+bool conv_win_fits(int N, int H, int W, int ks) {
+    return (ks == 3 || ks == 7) && W + 3 <= 1024 && conv_win_units(N, H, W, ks, 256) <= kWinLarge;
+}
 
 void launch_conv_win_x6(const X6Args& a, hipStream_t st) {
-    if (a.ks != 7 || a.small || a.pool || a.Mpad % 128 || !conv_win_fits(a.N, a.H, a.W))
+    if ((a.ks != 3 && a.ks != 7) || a.small || a.pool || a.Mpad % 128)
         throw std::invalid_argument("conv_win_x6: unsupported layer");
-    const int tiles = (a.Mpad / 128) * ((a.npix + 255) / 256) * a.ngroups;
-    hipLaunchKernelGGL((conv_win_x6<128, 256, 7, kWinMax>), dim3(tiles), dim3(512), 0, st, a);
+    const int need = conv_win_units(a.N, a.H, a.W, a.ks, 256);
+    const dim3 grid((a.Mpad / 128) * ((a.npix + 255) / 256) * a.ngroups), blk(512);
+    if (need <= kWinSmall) {
+        if (a.ks == 7) hipLaunchKernelGGL((conv_win_x6<128, 256, 7, kWinSmall>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL((conv_win_x6<128, 256, 3, kWinSmall>), grid, blk, 0, st, a);
+    } else if (need <= kWinLarge) {
+        if (a.ks == 7) hipLaunchKernelGGL((conv_win_x6<128, 256, 7, kWinLarge>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL((conv_win_x6<128, 256, 3, kWinLarge>), grid, blk, 0, st, a);
+    } else {
+        throw std::invalid_argument("conv_win_x6: window exceeds LDS");
+    }
 }
 
 }  // namespace opose

@@ -22,6 +22,7 @@
 //   fixup exactly as conv.hip.
 // * The epilogue adds bias, applies ReLU and writes the output split again (X6) into a
 //   group slice of a wider buffer (the CPM concat), or fp32 NCHW for the network outputs.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -510,13 +511,19 @@ static int grid_for(size_t total) {
     return (int)(b > 8192 ? 8192 : (b ? b : 1));
 }
 
-// Zero the padding units of `planes` X6P planes (common.h): the 3N + 4 rows outside the frames'
-// pixel rows and the 3 units before each of the N*H pixel rows.  One thread per padding unit.
-__global__ __launch_bounds__(256) void x6p_clear_pads_kernel(uint4* __restrict__ buf, size_t plane, int N, int H,
-                                                             int P, int planes) {
+// Zero the padding units of X6P buffers (common.h) of one geometry: per (piece, group) plane the
+// 3N + 4 rows outside the frames' pixel rows and the 3 units before each of the N*H pixel rows.
+// One launch for up to 8 buffers (blockIdx.y), one thread per padding unit.
+struct PadBufs {
+    uint4* p[8];
+    int planes[8];
+};
+
+__global__ __launch_bounds__(256) void x6p_clear_pads_kernel(PadBufs b, size_t plane, int N, int H, int P) {
     const int pad_rows = 3 * N + 4;
     const size_t per_plane = (size_t)pad_rows * P + (size_t)N * H * 3;
-    const size_t total = per_plane * planes;
+    uint4* buf = b.p[blockIdx.y];
+    const size_t total = per_plane * b.planes[blockIdx.y];
     const uint4 z = make_uint4(0u, 0u, 0u, 0u);
     for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
         const size_t pl = e / per_plane;
@@ -536,12 +543,20 @@ __global__ __launch_bounds__(256) void x6p_clear_pads_kernel(uint4* __restrict__
     }
 }
 
-void launch_x6p_clear_pads(uint8_t* buf, int planes, int N, int H, int W, hipStream_t st) {
+void launch_x6p_clear_pads(uint8_t* const* bufs, const int* planes, int nbufs, int N, int H, int W, hipStream_t st) {
+    if (nbufs < 1 || nbufs > 8) throw std::invalid_argument("x6p_clear_pads: 1..8 buffers");
     const int P = W + 3;
     const size_t plane = (size_t)(N * (H + 3) + 4) * P;
-    const size_t pads = ((size_t)(3 * N + 4) * P + (size_t)N * H * 3) * planes;
-    hipLaunchKernelGGL(x6p_clear_pads_kernel, dim3(grid_for(pads)), dim3(256), 0, st, reinterpret_cast<uint4*>(buf),
-                       plane, N, H, P, planes);
+    PadBufs b{};
+    int most = 0;
+    for (int i = 0; i < nbufs; ++i) {
+        b.p[i] = reinterpret_cast<uint4*>(bufs[i]);
+        b.planes[i] = planes[i];
+        most = std::max(most, planes[i]);
+    }
+    const size_t pads = ((size_t)(3 * N + 4) * P + (size_t)N * H * 3) * most;
+    hipLaunchKernelGGL(x6p_clear_pads_kernel, dim3(std::min(grid_for(pads), 2048), nbufs), dim3(256), 0, st, b, plane,
+                       N, H, P);
 }
 
 // fp32 NCHW channels [coff, coff + C) of cstride -> X6 groups [goff, goff + ceil(C/8)) of cg

@@ -137,7 +137,7 @@ struct DevConv {
     uint8_t* wx6 = nullptr;
     int nK6 = 0, cin_g = 0;
     bool small6 = false;
-    // 7x7 layers: the same weights in pair order for conv_win_x6 (conv_win.hip)
+    // 3x3 / 7x7 layers: the same weights in pair order for conv_win_x6 (conv_win.hip)
     uint8_t* wx6p = nullptr;
     int nK6p = 0;
     ~DevConv() {
@@ -201,8 +201,8 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_FIRST_DIRECT");
         return !(e && e[0] == '0');
     }();
-    // the batched 7x7 CPM convs by conv_win_x6 (input window in LDS; OPOSE_CONV7_WIN=0: conv_x6
-    // over the im2col stream, the cross-check of tests/test_gpu_x6.py)
+    // the batched 3x3 / 7x7 convs on padded inputs by conv_win_x6 (input window in LDS;
+    // OPOSE_CONV7_WIN=0: conv_x6 over the im2col stream, the cross-check of tests/test_gpu_x6.py)
     bool win7 = [] {
         const char* e = getenv("OPOSE_CONV7_WIN");
         return !(e && e[0] == '0');
@@ -218,7 +218,7 @@ struct opose_ctx {
     // network workspace, one set per concurrently running scale (slot s runs on scale_stream(s);
     // slot 0 is the handle's stream): input, activations, stream-K slabs
     struct NetWS {
-        DevBuf x, x6in, x6A, x6B, x6S0, x6S1, x6T0, x6T1, x6U, bufA, bufB, S0, S1, T0, T1, U, partial;
+        DevBuf x, x6in, x6A, x6B, x6P0, x6P1, x6Q0, x6Q1, x6S0, x6S1, x6T0, x6T1, x6U, bufA, bufB, S0, S1, T0, T1, U, partial;
     };
     NetWS ws[kMaxScales];
     int slot = 0;
@@ -472,7 +472,7 @@ static void upload_conv(opose_ctx* h, int net, const std::string& key, const std
         dc->small6 = dc->cin_g == 1;
         OPOSE_HIP_CHECK(hipMalloc(&dc->wx6, wx.size() * 2));
         OPOSE_HIP_CHECK(hipMemcpy(dc->wx6, wx.data(), wx.size() * 2, hipMemcpyHostToDevice));
-        if (s0.ks == 7 && dc->Mpad % 128 == 0) {
+        if ((s0.ks == 7 || s0.ks == 3) && dc->Mpad % 128 == 0 && cin_phys > 8) {
             x6_pack_weights_pairs(wp.data(), cout, cin_phys, s0.ks, dc->Mpad, &dc->nK6p, wx);
             OPOSE_HIP_CHECK(hipMalloc(&dc->wx6p, wx.size() * 2));
             OPOSE_HIP_CHECK(hipMemcpy(dc->wx6p, wx.data(), wx.size() * 2, hipMemcpyHostToDevice));
@@ -674,11 +674,11 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
         a.g[0].out2_l = dup.l;
     }
     if (ng == 1) a.g[1] = a.g[0];
-    // batched 7x7 layers on padded inputs: the LDS-window kernel over whole 128 x 256 tiles
-    // (>= 192 of them: a data-parallel grid that fills most of the chip)
+    // batched 3x3 / 7x7 layers on padded inputs: the LDS-window kernel over whole 128 x 256
+    // tiles (>= 192 of them: a data-parallel grid that fills most of the chip)
     const long win_tiles = (long)(a.Mpad / 128) * ((a.npix + 255) / 256) * ng;
-    if (h->win7 && c0->ks == 7 && c0->wx6p && (!c1 || c1->wx6p) && !pool && in0.padded && (!c1 || in1.padded) &&
-        win_tiles >= 192 && conv_win_fits(N, H, W)) {
+    if (h->win7 && c0->wx6p && (!c1 || c1->wx6p) && !pool && in0.padded && (!c1 || in1.padded) &&
+        win_tiles >= 192 && conv_win_fits(N, H, W, c0->ks)) {
         a.ngroups = ng;
         a.nK = c0->nK6p;
         a.g[0].wt = c0->wx6p;
@@ -688,7 +688,7 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
         for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)c0->K * a.npix;
         ProfEntry pe;
         h->prof_begin(pe, conv_class(c0->ks), flops, 0);
-        if (h->detail) pe.detail = "layer/" + c0->name + "/win7/s" + std::to_string(win_tiles) + "/n" + std::to_string(a.npix);
+        if (h->detail) pe.detail = "layer/" + c0->name + "/win/s" + std::to_string(win_tiles) + "/n" + std::to_string(a.npix);
         launch_conv_win_x6(a, h->stream);
         h->prof_end(pe);
         return;
@@ -710,18 +710,71 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
     h->prof_end(pe);
 }
 
-// VGG trunk on X6 activations: x fp32 [N,3,H,W] -> final trunk conv written via `last` (+ dup)
+// zero the padding units of X6P buffers of one geometry (cg groups each): the convs never write
+// them, but a forward of another geometry on the same workspace may have put pixels there.
+// One launch per geometry and forward (inside captured graphs too).
+static void clear_x6p_pads(opose_ctx* h, std::initializer_list<std::pair<uint8_t*, int>> bufs, int N, int H, int W) {
+    uint8_t* p[8];
+    int planes[8];
+    int n = 0;
+    for (const auto& b : bufs) {
+        p[n] = b.first;
+        planes[n] = 3 * b.second;
+        ++n;
+    }
+    ProfEntry pe;
+    h->prof_begin(pe, "x6p_pads", 0, 0);
+    launch_x6p_clear_pads(p, planes, n, N, H, W, h->stream);
+    h->prof_end(pe);
+}
+
+// VGG trunk on X6 activations: x fp32 [N,3,H,W] -> final trunk conv written via `last` (+ dup).
+// Full and half resolution run on dense X6 buffers (A / B); from the second pool on (H/4: conv3_x,
+// H/8: conv4_x, conv5_x of the hand) the activations are padded X6P (P0 / P1, Q0 / Q1), which the
+// windowed conv_win_x6 reads (conv_x6 reads either layout).
 static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, int W, XAct last, XAct dup) {
     const std::vector<Spec> vgg = net == OPOSE_NET_BODY ? vgg_body() : vgg_hand();
     const size_t npix = (size_t)N * H * W;
-    const size_t act = npix * 8 * 16 * 3;  // 64 channels at full resolution = the largest trunk tensor
+    const size_t act = npix * 8 * 16 * 3;  // 64 channels at full resolution = the largest dense tensor
     uint8_t* A = h->w().x6A.ensure<uint8_t>(act, h->stream);
     uint8_t* B = h->w().x6B.ensure<uint8_t>(act, h->stream);
-    uint8_t* cur = nullptr;
-    int cg = 1, hh = H, ww = W;
+    // padded levels (fused pooling only: the separate maxpool_x6 reads and writes dense X6)
+    const bool padded = h->fused_pool;
+    const int H4 = H / 4, W4 = W / 4, H8 = H / 8, W8 = W / 8;
+    int maxg4 = 0, maxg8 = 0;  // widest activation (groups) at H/4 and H/8
+    {
+        int lvl = 0;
+        for (const Spec& s : vgg) {
+            const int og = (s.cout + 7) / 8;
+            const bool pooled = s.name == "conv1_2" || s.name == "conv2_2" || s.name == "conv3_4";
+            const int out_lvl = lvl + (pooled ? 1 : 0);
+            if (out_lvl == 2) maxg4 = std::max(maxg4, og);
+            if (out_lvl == 3) maxg8 = std::max(maxg8, og);
+            lvl = out_lvl;
+        }
+    }
+    uint8_t *P0 = nullptr, *P1 = nullptr, *Q0 = nullptr, *Q1 = nullptr;
+    if (padded) {
+        P0 = h->w().x6P0.ensure<uint8_t>(x6p_plane(N, H4, W4) * maxg4 * 48, h->stream);
+        P1 = h->w().x6P1.ensure<uint8_t>(x6p_plane(N, H4, W4) * maxg4 * 48, h->stream);
+        Q0 = h->w().x6Q0.ensure<uint8_t>(x6p_plane(N, H8, W8) * maxg8 * 48, h->stream);
+        Q1 = h->w().x6Q1.ensure<uint8_t>(x6p_plane(N, H8, W8) * maxg8 * 48, h->stream);
+        clear_x6p_pads(h, {{P0, maxg4}, {P1, maxg4}}, N, H4, W4);
+        clear_x6p_pads(h, {{Q0, maxg8}, {Q1, maxg8}}, N, H8, W8);
+    }
+    // output buffer for a layer at resolution level `lvl` (0: H, 1: H/2, 2: H/4, 3: H/8), not `avoid`
+    auto out_buf = [&](int lvl, int og, const void* avoid) -> XAct {
+        const int hh = H >> lvl, ww = W >> lvl;
+        if (!padded || lvl < 2) return x6act(avoid == A ? B : A, og, 0, N, hh, ww);
+        uint8_t* p = lvl == 2 ? (avoid == P0 ? P1 : P0) : (avoid == Q0 ? Q1 : Q0);
+        return x6pact(p, og, 0, N, hh, ww);
+    };
+    XAct cur;
+    int lvl = 0;
     for (size_t i = 0; i < vgg.size(); ++i) {
         const Spec& s = vgg[i];
         DevConv* c = find_conv(h, net, s.name);
+        const int hh = H >> lvl, ww = W >> lvl;
         if (i == 0 && s.cin == 3 && s.cout == 64 && s.ks == 3 && s.pad == 1 && vgg.size() > 1 && h->first_direct) {
             // conv1_1 straight from the fp32 input (conv_first_x6), no input split
             ProfEntry pe;
@@ -729,8 +782,7 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
             if (h->detail) pe.detail = "layer/" + s.name + "/first_direct/n" + std::to_string(npix);
             launch_conv_first_x6(x, N, 3, H, W, c->wt, c->Mpad, c->bias, A, (uint32_t)(npix * 8 * 16), h->stream);
             h->prof_end(pe);
-            cur = A;
-            cg = 8;
+            cur = x6act(A, 8, 0, N, H, W);
             continue;
         }
         if (i == 0) {
@@ -739,67 +791,49 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
             h->prof_begin(pe, "to_x6", 0, (double)npix * (12 + 48));
             launch_to_x6(x, 3, 0, 3, N, H * W, X, 1, 0, (uint32_t)(npix * 16), h->stream);
             h->prof_end(pe);
-            cur = X;
+            cur = x6act(X, 1, 0, N, H, W);
         }
         const bool final_layer = i + 1 == vgg.size();
-        uint8_t* dst = (cur == A) ? B : A;
         const int og = (s.cout + 7) / 8;
-        const size_t np = (size_t)N * hh * ww;
         const bool pooled = s.name == "conv1_2" || s.name == "conv2_2" || s.name == "conv3_4";
-        if (pooled && h->fused_pool && h->win12 && s.name == "conv1_2" && cg == 8 && c->cin == 64 &&
-            c->cout == 64 && c->ks == 3 && c->pad == 1 && c->Mpad == 64 && c->nK6 == 18 && !c->small6) {
+        if (pooled && h->fused_pool && h->win12 && s.name == "conv1_2" && !cur.padded && cur.l.fs == 8u * hh * ww &&
+            c->cin == 64 && c->cout == 64 && c->ks == 3 && c->pad == 1 && c->Mpad == 64 && c->nK6 == 18 &&
+            !c->small6) {
             // conv1_2 + pool with the input window in LDS instead of the 9-tap im2col stream
-            const size_t npo = (size_t)N * (hh / 2) * (ww / 2);
+            const size_t np = (size_t)N * hh * ww, npo = (size_t)N * (hh / 2) * (ww / 2);
+            const XAct out = out_buf(lvl + 1, og, cur.p);
             ProfEntry pe;
             h->prof_begin(pe, "conv3x3", 2.0 * 64 * 576 * (double)(npo * 4), 0);
             if (h->detail) pe.detail = "layer/" + s.name + "/x6win/n" + std::to_string(npo * 4);
-            launch_conv3_pool_win_x6(cur, (uint32_t)(np * 8 * 16), N, hh, ww, c->wx6, c->bias, dst,
-                                     (uint32_t)(npo * 8 * 16), h->stream);
+            launch_conv3_pool_win_x6(static_cast<const uint8_t*>(cur.p), (uint32_t)(np * 8 * 16), N, hh, ww, c->wx6,
+                                     c->bias, static_cast<uint8_t*>(out.p), (uint32_t)(npo * 8 * 16), h->stream);
             h->prof_end(pe);
-            cur = dst;
-            cg = og;
-            hh /= 2;
-            ww /= 2;
+            cur = out;
+            ++lvl;
             continue;
         }
         if (pooled && h->fused_pool) {  // conv + MaxPool2d(2, 2) in one launch
-            run_conv_x6(h, c, nullptr, N, hh, ww, x6act(cur, cg, 0, N, hh, ww), x6act(dst, og, 0, N, hh / 2, ww / 2),
-                        XAct{}, XAct{}, true, false, XAct{}, true);
-            cur = dst;
-            cg = og;
-            hh /= 2;
-            ww /= 2;
+            const XAct out = out_buf(lvl + 1, og, cur.p);
+            run_conv_x6(h, c, nullptr, N, hh, ww, cur, out, XAct{}, XAct{}, true, false, XAct{}, true);
+            cur = out;
+            ++lvl;
             continue;
         }
-        XAct out = final_layer ? last : x6act(dst, og, 0, N, hh, ww);
-        run_conv_x6(h, c, nullptr, N, hh, ww, x6act(cur, cg, 0, N, hh, ww), out, XAct{}, XAct{}, true, false,
-                    final_layer ? dup : XAct{});
-        cur = dst;
-        cg = og;
-        if (pooled) {
-            uint8_t* pd = (cur == A) ? B : A;
+        const XAct out = final_layer ? last : out_buf(lvl, og, cur.p);
+        run_conv_x6(h, c, nullptr, N, hh, ww, cur, out, XAct{}, XAct{}, true, false, final_layer ? dup : XAct{});
+        cur = out;
+        if (pooled) {  // separate MaxPool2d(2, 2) (fused_pool off: dense buffers throughout)
+            const size_t np = (size_t)N * hh * ww;
+            const XAct pd = x6act(cur.p == A ? B : A, og, 0, N, hh / 2, ww / 2);
             ProfEntry pe;
-            h->prof_begin(pe, "maxpool", 0, (double)np * cg * 48 * 1.25);
-            launch_maxpool_x6(cur, (uint32_t)(np * cg * 16), pd, (uint32_t)((size_t)N * (hh / 2) * (ww / 2) * cg * 16),
-                              N * cg, hh, ww, h->stream);
+            h->prof_begin(pe, "maxpool", 0, (double)np * og * 48 * 1.25);
+            launch_maxpool_x6(static_cast<const uint8_t*>(cur.p), (uint32_t)(np * og * 16), static_cast<uint8_t*>(pd.p),
+                              (uint32_t)((size_t)N * (hh / 2) * (ww / 2) * og * 16), N * og, hh, ww, h->stream);
             h->prof_end(pe);
-            hh /= 2;
-            ww /= 2;
             cur = pd;
+            ++lvl;
         }
     }
-}
-
-// zero the padding units of the X6P stage buffers (two sets of two buffers): the convs never write
-// them, but a forward of another geometry on the same workspace may have put pixels there.
-// Launched every forward (inside captured graphs too): ~10 us per 32-frame bench step.
-static void clear_x6p_pads(opose_ctx* h, std::initializer_list<uint8_t*> s, int sg, std::initializer_list<uint8_t*> t,
-                           int tg, int N, int H, int W) {
-    ProfEntry pe;
-    h->prof_begin(pe, "x6p_pads", 0, 0);
-    for (uint8_t* p : s) launch_x6p_clear_pads(p, 3 * sg, N, H, W, h->stream);
-    for (uint8_t* p : t) launch_x6p_clear_pads(p, 3 * tg, N, H, W, h->stream);
-    h->prof_end(pe);
 }
 
 // bodypose_model.forward on X6 activations; output fp32 in S0 with the fp32 path's layout
@@ -816,7 +850,7 @@ static float* body_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
                      h->w().x6T1.ensure<uint8_t>(plane * TG * 48, h->stream)};
     uint8_t* U = h->w().x6U.ensure<uint8_t>(px * UG * 48, h->stream);
     float* O = h->w().S0.ensure<float>(px * 185, h->stream);
-    clear_x6p_pads(h, {S[0], S[1]}, SG, {T[0], T[1]}, TG, N, hl, wl);
+    clear_x6p_pads(h, {{S[0], SG}, {S[1], SG}, {T[0], TG}, {T[1], TG}}, N, hl, wl);
     const int net = OPOSE_NET_BODY;
     auto s_ = [&](int i, int goff) { return x6pact(S[i], SG, goff, N, hl, wl); };
     auto t_ = [&](int i, int goff) { return x6pact(T[i], TG, goff, N, hl, wl); };
@@ -865,7 +899,7 @@ static float* hand_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
                      h->w().x6T1.ensure<uint8_t>(plane * TG * 48, h->stream)};
     uint8_t* U = h->w().x6U.ensure<uint8_t>(px * UG * 48, h->stream);
     float* O = h->w().S0.ensure<float>(px * 150, h->stream);
-    clear_x6p_pads(h, {S[0], S[1]}, SG, {T[0], T[1]}, TG, N, hl, wl);
+    clear_x6p_pads(h, {{S[0], SG}, {S[1], SG}, {T[0], TG}, {T[1], TG}}, N, hl, wl);
     const int net = OPOSE_NET_HAND;
     auto s_ = [&](int i, int goff) { return x6pact(S[i], SG, goff, N, hl, wl); };
     auto t_ = [&](int i) { return x6pact(T[i], TG, 0, N, hl, wl); };

@@ -37,7 +37,7 @@ void launch_from_x6(const uint8_t* in, int cg, int goff, uint32_t ps, int C, int
 void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const float* wt, int Mpad, const float* bias,
                           uint8_t* out, uint32_t ops, hipStream_t st);
 // zero the padding units of `planes` X6P (piece, group) planes of an N x H x W buffer (common.h)
-void launch_x6p_clear_pads(uint8_t* buf, int planes, int N, int H, int W, hipStream_t st);
+void launch_x6p_clear_pads(uint8_t* const* bufs, const int* planes, int nbufs, int N, int H, int W, hipStream_t st);
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,
                        hipStream_t st);
 // conv1_2 (64 -> 64, 3x3 pad 1) + MaxPool2d(2, 2) from an 8-group X6 tensor, input window in LDS
@@ -47,7 +47,7 @@ void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int
 // input (pair-order weights: x6_pack_weights_pairs); whole 128 x 256 tiles
 void x6_pack_weights_pairs(const float* w, int cout, int cin, int ks, int Mpad, int* nK_out,
                            std::vector<uint16_t>& out);
-bool conv_win_fits(int N, int H, int W);
+bool conv_win_fits(int N, int H, int W, int ks);
 void launch_conv_win_x6(const X6Args& a, hipStream_t st);
 // imgproc.hip
 void launch_preprocess(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int Hs,
