@@ -102,6 +102,7 @@ std::atomic<uint64_t> g_alloc_epoch{1};
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    uint64_t pad_key = 0;  // X6P geometry whose padding units are known zero (0: none)
     ~DevBuf() {
         if (p) (void)hipFree(p);
     }
@@ -118,6 +119,7 @@ struct DevBuf {
             size_t nb = std::max(b, bytes + bytes / 4);
             OPOSE_HIP_CHECK(hipMalloc(&p, nb));
             bytes = nb;
+            pad_key = 0;
             g_alloc_epoch.fetch_add(1);
         }
         return static_cast<T*>(p);
@@ -675,10 +677,13 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
     }
     if (ng == 1) a.g[1] = a.g[0];
     // batched 3x3 / 7x7 layers on padded inputs: the LDS-window kernel over whole 128 x 256
-    // tiles (>= 192 of them: a data-parallel grid that fills most of the chip)
+    // tiles, when the data-parallel grid fills the chip's 256 CUs in its rounds (>= 85 %: 236,
+    // 472 and 944 tiles on the bench; a hand crop's 266 tiles would leave the second round
+    // nearly empty -- conv_x6 balances such layers by stream-K)
     const long win_tiles = (long)(a.Mpad / 128) * ((a.npix + 255) / 256) * ng;
+    const double win_fill = (double)win_tiles / (double)(((win_tiles + 255) / 256) * 256);
     if (h->win7 && c0->wx6p && (!c1 || c1->wx6p) && !pool && in0.padded && (!c1 || in1.padded) &&
-        win_tiles >= 192 && conv_win_fits(N, H, W, c0->ks)) {
+        win_tiles >= 192 && win_fill >= 0.85 && conv_win_fits(N, H, W, c0->ks)) {
         a.ngroups = ng;
         a.nK = c0->nK6p;
         a.g[0].wt = c0->wx6p;
@@ -710,22 +715,42 @@ static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, in
     h->prof_end(pe);
 }
 
-// zero the padding units of X6P buffers of one geometry (cg groups each): the convs never write
-// them, but a forward of another geometry on the same workspace may have put pixels there.
-// One launch per geometry and forward (inside captured graphs too).
-static void clear_x6p_pads(opose_ctx* h, std::initializer_list<std::pair<uint8_t*, int>> bufs, int N, int H, int W) {
+// Zero the padding units of X6P buffers (cg groups each) for an N x H x W geometry.  The convs
+// never write them, so a buffer stays valid for its geometry until a forward of another geometry
+// writes pixels where this one has pads: clear only on a geometry change (or a reallocation),
+// and then invalidate the captured graphs, whose replays assume their own geometry's pads are
+// zero.  Inside a stream capture the clear becomes part of the graph (replayed every time) and
+// the keys stay unset.
+static void clear_x6p_pads(opose_ctx* h, std::initializer_list<std::pair<DevBuf*, int>> bufs, int N, int H, int W) {
     uint8_t* p[8];
     int planes[8];
+    DevBuf* owner[8];
     int n = 0;
     for (const auto& b : bufs) {
-        p[n] = b.first;
+        const uint64_t key = ((uint64_t)N << 40) ^ ((uint64_t)H << 20) ^ (uint64_t)W ^ ((uint64_t)b.second << 58) ^ 1u;
+        if (b.first->pad_key == key) continue;
+        p[n] = static_cast<uint8_t*>(b.first->p);
         planes[n] = 3 * b.second;
+        owner[n] = b.first;
         ++n;
     }
+    if (!n) return;
     ProfEntry pe;
     h->prof_begin(pe, "x6p_pads", 0, 0);
     launch_x6p_clear_pads(p, planes, n, N, H, W, h->stream);
     h->prof_end(pe);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    OPOSE_HIP_CHECK(hipStreamIsCapturing(h->stream, &cs));
+    if (cs != hipStreamCaptureStatusNone) return;
+    int i = 0;
+    for (const auto& b : bufs) {
+        const uint64_t key = ((uint64_t)N << 40) ^ ((uint64_t)H << 20) ^ (uint64_t)W ^ ((uint64_t)b.second << 58) ^ 1u;
+        if (i < n && owner[i] == b.first) {
+            b.first->pad_key = key;
+            ++i;
+        }
+    }
+    g_alloc_epoch.fetch_add(1);
 }
 
 // VGG trunk on X6 activations: x fp32 [N,3,H,W] -> final trunk conv written via `last` (+ dup).
@@ -759,8 +784,8 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
         P1 = h->w().x6P1.ensure<uint8_t>(x6p_plane(N, H4, W4) * maxg4 * 48, h->stream);
         Q0 = h->w().x6Q0.ensure<uint8_t>(x6p_plane(N, H8, W8) * maxg8 * 48, h->stream);
         Q1 = h->w().x6Q1.ensure<uint8_t>(x6p_plane(N, H8, W8) * maxg8 * 48, h->stream);
-        clear_x6p_pads(h, {{P0, maxg4}, {P1, maxg4}}, N, H4, W4);
-        clear_x6p_pads(h, {{Q0, maxg8}, {Q1, maxg8}}, N, H8, W8);
+        clear_x6p_pads(h, {{&h->w().x6P0, maxg4}, {&h->w().x6P1, maxg4}}, N, H4, W4);
+        clear_x6p_pads(h, {{&h->w().x6Q0, maxg8}, {&h->w().x6Q1, maxg8}}, N, H8, W8);
     }
     // output buffer for a layer at resolution level `lvl` (0: H, 1: H/2, 2: H/4, 3: H/8), not `avoid`
     auto out_buf = [&](int lvl, int og, const void* avoid) -> XAct {
@@ -850,7 +875,7 @@ static float* body_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
                      h->w().x6T1.ensure<uint8_t>(plane * TG * 48, h->stream)};
     uint8_t* U = h->w().x6U.ensure<uint8_t>(px * UG * 48, h->stream);
     float* O = h->w().S0.ensure<float>(px * 185, h->stream);
-    clear_x6p_pads(h, {{S[0], SG}, {S[1], SG}, {T[0], TG}, {T[1], TG}}, N, hl, wl);
+    clear_x6p_pads(h, {{&h->w().x6S0, SG}, {&h->w().x6S1, SG}, {&h->w().x6T0, TG}, {&h->w().x6T1, TG}}, N, hl, wl);
     const int net = OPOSE_NET_BODY;
     auto s_ = [&](int i, int goff) { return x6pact(S[i], SG, goff, N, hl, wl); };
     auto t_ = [&](int i, int goff) { return x6pact(T[i], TG, goff, N, hl, wl); };
@@ -899,7 +924,7 @@ static float* hand_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
                      h->w().x6T1.ensure<uint8_t>(plane * TG * 48, h->stream)};
     uint8_t* U = h->w().x6U.ensure<uint8_t>(px * UG * 48, h->stream);
     float* O = h->w().S0.ensure<float>(px * 150, h->stream);
-    clear_x6p_pads(h, {{S[0], SG}, {S[1], SG}, {T[0], TG}, {T[1], TG}}, N, hl, wl);
+    clear_x6p_pads(h, {{&h->w().x6S0, SG}, {&h->w().x6S1, SG}, {&h->w().x6T0, TG}, {&h->w().x6T1, TG}}, N, hl, wl);
     const int net = OPOSE_NET_HAND;
     auto s_ = [&](int i, int goff) { return x6pact(S[i], SG, goff, N, hl, wl); };
     auto t_ = [&](int i) { return x6pact(T[i], TG, 0, N, hl, wl); };
