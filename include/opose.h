@@ -122,6 +122,12 @@ int opose_body_forward(opose_t* h, const float* x, int N, int Hp, int Wp,
                        float* paf, float* heat, int flags);
 /* heat [N,22,Hp/8,Wp/8] */
 int opose_hand_forward(opose_t* h, const float* x, int N, int Hp, int Wp, float* heat, int flags);
+/* The networks of a scale pyramid in one lockstep pass, as Hand() runs them (src/hand.py:33-57
+ * evaluates self.model once per scale_search entry): xs[i] [N[i],3,Hp[i],Wp[i]] -> heats[i]
+ * [N[i],22,Hp[i]/8,Wp[i]/8], i < n <= OPOSE_MAX_SCALES; one conv launch per layer covers
+ * every scale (split-bf16 path; the fp32 path runs the scales one after another). */
+int opose_hand_forward_pyramid(opose_t* h, int n, const float* const* xs, const int* N, const int* Hp,
+                               const int* Wp, float* const* heats, int flags);
 
 /* ---- end to end ---------------------------------------------------------------------- */
 /* bgr: N frames uint8 [H][W][3] (row stride `row_stride` bytes, frame stride

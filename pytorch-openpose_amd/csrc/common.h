@@ -77,15 +77,25 @@ struct X6Group {
     X6Layout in_l, out_l, out2_l;     // unit addressing of the X6 slices
     int out_c, out_off;    // fp32 output: channels per frame / first channel
     int cout, relu, out_f32;
+    int N, H, W;           // this group's frames (stride-1 'same' conv; pooled: the input's H, W)
+    int npix;              // GEMM columns: N*H*W (pooled: N*(H/2)*(W/2)*4, quad-major)
+    int t0;                // first tile of the group in the launch's tile space (set by the launcher)
 };
 
+// One launch runs up to kX6Groups GEMMs of the same conv shape (ks, Cin, Mpad): the two CPM
+// branches of a stage, and the scales of a pyramid (Hand()'s four, C5's) -- a "segment" per
+// (scale, branch), each with its own geometry and buffers.  Tiles are numbered group after
+// group (t0), so one data-parallel or stream-K grid covers all of them.
+constexpr int kX6Groups = 8;
+
 struct X6Args {
-    X6Group g[2];
-    int N, H, W, ks, pad;
+    X6Group g[kX6Groups];
+    int ks, pad;
     int cin_g;      // channel groups of the conv's input (Cin padded to 8)
     int small;      // 1: one group (Cin <= 8), chunks of 4 taps; 0: chunks of (4 groups, 1 tap)
     int nK;         // chunks of 32 k
-    int Mpad, npix, ngroups, sk_grid;
+    int Mpad, ngroups, sk_grid;
+    int tiles;      // tiles of all groups (set by the launcher)
     float* partial; // stream-K partial slabs [2 * sk_grid][MT * PT]
     int pool;       // 1: 2x2/2 max-pool fused into the epilogue (npix = N * (H/2) * (W/2) * 4, quad-major)
 };

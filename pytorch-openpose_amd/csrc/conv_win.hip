@@ -17,8 +17,12 @@
 //  * Everything else is conv_x6's MODE-2 loop: 128 x 256 tile, 8 waves of 64 x 64, weights by
 //    LDS-DMA into two stages, six piece products per chunk in the order
 //    (0,2) (0,0) (0,1) | barrier | (1,0) (2,0) (1,1), fragments refilled after their last use.
-//  * Whole tiles only (data-parallel grid of >= ~200 tiles: the batched path); the host falls
-//    back to conv_x6 (stream-K) for small problems and when a window would exceed WMAX.
+//  * Data-parallel grids (one workgroup per tile) or stream-K ranges over (tile, chunk) with
+//    conv_x6's partial slabs and fixup; a range may start inside a channel group (its first two
+//    windows are loaded in the prologue).  The host falls back to conv_x6 when a window would
+//    exceed WMAX.
+//  * The groups of a launch (X6Group: CPM branches, pyramid scales) each carry their own
+//    geometry; a tile's window and pixels come from its group.
 //  * The same kernel runs the batched 3x3 convs on padded inputs (trunk conv3_x / conv4_x and
 //    the stage-1 CPM convs, src/model.py:41-62): a window per group serves 9 taps.
 #include <algorithm>
@@ -51,24 +55,33 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
+    const int nM = a.Mpad / MT;
     const int nK = a.nK;
-    const int H = a.H, W = a.W, HW = H * W;
     const int wm0 = (wave % NWM) * WM;
     const int wp0 = (wave / NWM) * WP;
 
-    int tile;
+    // stream-K range of this workgroup over (tile, chunk), XCD-contiguous (guide T1); a grid of
+    // one workgroup per tile is the data-parallel case.  Pieces run from the range end backwards.
+    const int Gw = gridDim.x;
+    int id;
     {
-        const int Gw = gridDim.x, b = blockIdx.x;
-        const int q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
-        tile = xcd * q + min(xcd, rr) + (b >> 3);  // XCD-contiguous tiles (guide T1)
+        const int b = blockIdx.x, q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
+        id = xcd * q + min(xcd, rr) + (b >> 3);
     }
-    const int mt = tile % nM;
-    const int rest = tile / nM;
-    const int ptl = rest % nP;
-    const int gsel = rest / nP;
-    const X6Group G = gsel == 0 ? a.g[0] : a.g[1];
+    const long long I = (long long)a.tiles * nK;
+    const long long lo = (long long)id * I / Gw, hi = (long long)(id + 1) * I / Gw;
+    for (long long itp = hi; itp > lo;) {
+    const int tile = (int)((itp - 1) / nK);
+    const int c_end = (int)(itp - (long long)tile * nK);
+    const int c_begin = (int)max<long long>(0, lo - (long long)tile * nK);
+    itp = (long long)tile * nK + c_begin;
+    const int first = itp == lo;
+    const X6Group& G = a.g[x6_group_of(a, tile)];
+    const int H = G.H, W = G.W, HW = H * W, npix = G.npix;
+    const int mt = (tile - G.t0) % nM;
+    const int ptl = (tile - G.t0) / nM;
     const int p0 = ptl * PT, m0 = mt * MT;
+    __syncthreads();  // the previous piece's LDS reads are done
     if (tid < MT) s_bias[tid] = (m0 + tid < G.cout) ? G.bias[m0 + tid] : 0.f;
 
     // ---- window geometry (wave-uniform): padded rows R of the tile's first / last pixel
@@ -77,7 +90,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
         const int n = p / HW, y = (p - n * HW) / W;
         return 3 + n * (H + 3) + y;
     };
-    const int p_last = min(p0 + PT, a.npix) - 1;
+    const int p_last = min(p0 + PT, npix) - 1;
     const int R0 = prow(p0), R1 = prow(p_last);
     const int ws = (R0 - PAD) * P;                                // window start (unit of the plane)
     const int L = (R1 - R0 + 2 * PAD + 1) * P + PAD;              // units the taps can touch
@@ -118,13 +131,13 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     uint32_t bbase[TN];  // LDS byte address of the lane's pixel unit (window buffer 0, piece 0)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-        const int p = min(p0 + wp0 + 16 * j + (lane & 15), a.npix - 1);  // past the end: any window unit
+        const int p = min(p0 + wp0 + 16 * j + (lane & 15), npix - 1);  // past the end: any window unit
         const int n = p / HW, r = p - n * HW, y = r / W, x = r - y * W;
         const int wpos = (3 + n * (H + 3) + y) * P + 3 + x - ws;
         bbase[j] = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + 2 * A_U + wpos);
     }
     // pair of this lane's k-group in a chunk: q = 4c + gi -> (group g, tap t), advanced by 4 per chunk
-    int pg_g = 0, pg_t = gi;  // chunk 0
+    int pg_g = (4 * c_begin + gi) / TAPS, pg_t = (4 * c_begin + gi) % TAPS;  // chunk c_begin
     auto pair_off = [&]() __attribute__((always_inline)) -> uint32_t {
         const int g = min(pg_g, cin_g - 1);  // padded pairs past the last group: its data (weights 0)
         const int ky = pg_t / KS;
@@ -180,11 +193,13 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
         }
     };
 
-    // ---- prologue: windows of groups 0 and 1, weight stages of chunks 0 and 1
-    dma_win(0);
-    if (cin_g > 1) dma_win(1);
-    dma_a(0, 0);
-    dma_a(min(1, nK - 1), 1);
+    // ---- prologue: windows of the first two groups the range reads, weight stages of its first
+    // two chunks
+    const int g_first = (4 * c_begin) / TAPS;
+    dma_win(g_first);
+    if (g_first + 1 < cin_g) dma_win(g_first + 1);
+    dma_a(c_begin, 0);
+    dma_a(min(c_begin + 1, c_end - 1), 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // both windows and both stages landed everywhere
     uint32_t bcur[TN], bnxt[TN];
@@ -199,12 +214,12 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
         for (int r = 0; r < TMN; ++r) rd(1, r, a0, bnxt);
     }
     // group whose last chunk comes next, and that chunk: its buffer is refilled after that barrier
-    int end_g = 0;
-    int end_c = (TAPS - 1) / 4;
-    for (int c = 0; c < nK; ++c) {
-        const int buf = c & 1;
+    int end_g = g_first;
+    int end_c = (g_first * TAPS + TAPS - 1) / 4;
+    for (int c = c_begin; c < c_end; ++c) {
+        const int buf = (c - c_begin) & 1;
         const uint32_t a_cur = la(buf), a_nxt = la(buf ^ 1);
-        const int c2 = min(c + 2, nK - 1);  // past the end: a harmless reload of the last chunk
+        const int c2 = min(c + 2, c_end - 1);  // past the end: a harmless reload of the last chunk
 #pragma unroll
         for (int j = 0; j < TN; ++j) bcur[j] = bnxt[j];
         advance();  // (pg_g, pg_t) -> chunk c + 1
@@ -290,12 +305,29 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the last (unused) reads / loads landed
     fence_all();
 
-    // ---- epilogue (conv_x6's, whole tiles): bias + ReLU, X6 / X6P slices or fp32 NCHW
+    // ---- epilogue: a piece of a shared tile leaves an fp32 partial slab (summed in k order by
+    // conv_x6_fixup); a whole tile adds bias + ReLU and writes X6 / X6P slices or fp32 NCHW
+    if (c_begin != 0 || c_end != nK) {
+        float* slab = a.partial + (size_t)(2 * id + (first ? 0 : 1)) * (MT * PT);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int pl = wp0 + j * 16 + (lane & 15);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int ml = wm0 + i * 16 + 4 * (lane >> 4) + t;
+                    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(slab + ml * PT + pl), "v"(acc[i][j][t])
+                                 : "memory");
+                }
+        }
+        continue;
+    }
     const int cout8 = (G.cout + 7) & ~7;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int p = p0 + wp0 + j * 16 + (lane & 15);
-        if (p >= a.npix) continue;
+        if (p >= npix) continue;
         const int n = p / HW;
         const int rem = p - n * HW;
         const int y = rem / W, x = rem - y * W;
@@ -324,6 +356,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
             }
         }
     }
+    }  // pieces
 }
 
 // weights [cout][cin][ks][ks] (fp32, physical input channel order) -> X6 chunks in pair order:
@@ -387,11 +420,19 @@ bool conv_win_fits(int N, int H, int W, int ks) {
     return (ks == 3 || ks == 7) && W + 3 <= 1024 && conv_win_units(N, H, W, ks, 256) <= kWinLarge;
 }
 
-void launch_conv_win_x6(const X6Args& a, hipStream_t st) {
-    if ((a.ks != 3 && a.ks != 7) || a.small || a.pool || a.Mpad % 128)
+void launch_conv_win_x6(const X6Args& a0, hipStream_t st) {
+    if ((a0.ks != 3 && a0.ks != 7) || a0.small || a0.pool || a0.Mpad % 128)
         throw std::invalid_argument("conv_win_x6: unsupported layer");
-    const int need = conv_win_units(a.N, a.H, a.W, a.ks, 256);
-    const dim3 grid((a.Mpad / 128) * ((a.npix + 255) / 256) * a.ngroups), blk(512);
+    const X6Args a = x6_number_tiles(a0, 128, 256);
+    int need = 0;
+    for (int g = 0; g < a.ngroups; ++g) {
+        const X6Group& G = a.g[g];
+        if (G.in_l.rs != (uint32_t)G.W + 3 || G.in_l.fs != (uint32_t)(G.H + 3) * G.in_l.rs)
+            throw std::invalid_argument("conv_win_x6: input is not X6P");
+        need = std::max(need, conv_win_units(G.N, G.H, G.W, a.ks, 256));
+    }
+    if (a.sk_grid < 1 || a.sk_grid > a.tiles * a.nK) throw std::invalid_argument("conv_win_x6: bad grid");
+    const dim3 grid(a.sk_grid), blk(512);
     if (need <= kWinSmall) {
         if (a.ks == 7) hipLaunchKernelGGL((conv_win_x6<128, 256, 7, kWinSmall>), grid, blk, 0, st, a);
         else hipLaunchKernelGGL((conv_win_x6<128, 256, 3, kWinSmall>), grid, blk, 0, st, a);
@@ -401,6 +442,7 @@ void launch_conv_win_x6(const X6Args& a, hipStream_t st) {
     } else {
         throw std::invalid_argument("conv_win_x6: window exceeds LDS");
     }
+    if (a.sk_grid != a.tiles) launch_conv_x6_fixup(a, 128, 256, st);
 }
 
 }  // namespace opose

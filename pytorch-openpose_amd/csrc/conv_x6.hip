@@ -64,19 +64,20 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
+    const int nM = a.Mpad / MT;
     const int nK = a.nK;
-    const int HW = a.H * a.W;
+    // geometry of the current tile's group (X6Group N, H, W, npix)
+    int H = 0, W = 0, HW = 0, npix = 0;
     // pooled conv (a.pool): GEMM columns run over the 2x2 quads of the pooled grid, quad-major
     // (column q -> pooled pixel q >> 2, quadrant q & 3), so the epilogue pools 4 adjacent lanes
-    const int Wo = a.W >> 1, HWo = (a.H >> 1) * Wo;
+    int Wo = 0, HWo = 0;
     auto decode = [&](int p, int& n, int& r) __attribute__((always_inline)) {  // column -> frame, y*W+x
         if (a.pool) {
             const int q = p >> 2, d = p & 3;
             n = q / HWo;
             const int ro = q - n * HWo;
             const int yo = ro / Wo;
-            r = (2 * yo + (d >> 1)) * a.W + 2 * (ro - yo * Wo) + (d & 1);
+            r = (2 * yo + (d >> 1)) * W + 2 * (ro - yo * Wo) + (d & 1);
         } else {
             n = p / HW;
             r = p - n * HW;
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int b = blockIdx.x;
     const int q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
     const int id = xcd * q + min(xcd, rr) + (b >> 3);
-    const long long I = (long long)nM * nP * a.ngroups * nK;
+    const long long I = (long long)a.tiles * nK;
     const long long lo = (long long)id * I / Gw, hi = (long long)(id + 1) * I / Gw;
 
     for (long long itp = hi; itp > lo;) {
@@ -100,11 +101,15 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         const int c_begin = (int)max<long long>(0, lo - (long long)tile * nK);
         itp = (long long)tile * nK + c_begin;
         const int first = itp == lo;
-        const int mt = tile % nM;
-        const int rest = tile / nM;
-        const int pt = rest % nP;
-        const int g = rest / nP;
-        const X6Group G = g == 0 ? a.g[0] : a.g[1];
+        const X6Group& G = a.g[x6_group_of(a, tile)];
+        H = G.H;
+        W = G.W;
+        HW = H * W;
+        npix = G.npix;
+        Wo = W >> 1;
+        HWo = (H >> 1) * Wo;
+        const int mt = (tile - G.t0) % nM;
+        const int pt = (tile - G.t0) / nM;
         const int p0 = pt * PT;
         const int m0 = mt * MT;
 
@@ -117,11 +122,11 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         uint32_t pbase;
         {
             const int p = p0 + jw * 64 + lane;
-            const bool v = p < a.npix;
+            const bool v = p < npix;
             int n, r;
             decode(v ? p : 0, n, r);
-            const int y = r / a.W;
-            px = r - y * a.W;
+            const int y = r / W;
+            px = r - y * W;
             py = v ? y : -100000;
             pbase = (n * G.in_l.fs + (uint32_t)y * G.in_l.rs + (uint32_t)px) * 16u;
         }
@@ -138,7 +143,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             const int ky = tap / ks;
             const int dy = ky - a.pad, dx = tap - ky * ks - a.pad;
             const int iy = py + dy, ix = px + dx;
-            const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+            const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
             return ok ? pbase + (uint32_t)((dy * (int)G.in_l.rs + dx) * 16) : 0x80000000u;  // >= num_records -> 0
         };
         // im2col DMA of chunk c, unit u of this wave ((piece, group) row pg0 + u * WPJ) into stage buf;
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
                 const int n = q / HWo;
                 const int remo = q - n * HWo;
                 const int yo = remo / Wo, xo = remo - yo * Wo;
-                const bool lead = (lane & 3) == 0 && p < a.npix;
+                const bool lead = (lane & 3) == 0 && p < npix;
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -407,10 +412,10 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
                     }
                 continue;
             }
-            if (p >= a.npix) continue;
+            if (p >= npix) continue;
             const int n = p / HW;
             const int rem = p - n * HW;
-            const int y = rem / a.W, x = rem - y * a.W;
+            const int y = rem / W, x = rem - y * W;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -448,28 +453,26 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
 // a group) of one pixel of a shared tile: partial slabs summed in k order (deterministic).
 template <int MT, int PT>
 __global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
-    const int nM = a.Mpad / MT, nP = (a.npix + PT - 1) / PT;
+    const int nM = a.Mpad / MT;
     const int nK = a.nK;
     const long long Gw = a.sk_grid;
-    const long long I = (long long)nM * nP * a.ngroups * nK;
+    const long long I = (long long)a.tiles * nK;
     const int tile = blockIdx.x;
     const long long x0 = (long long)tile * nK;
     const int w0 = (int)(((x0 + 1) * Gw - 1) / I);
     const int w1 = (int)(((x0 + nK) * Gw - 1) / I);
     if (w0 == w1) return;
-    const int mt = tile % nM;
-    const int rest = tile / nM;
-    const int pt = rest % nP;
-    const int g = rest / nP;
-    const X6Group G = g == 0 ? a.g[0] : a.g[1];
-    const int HW = a.H * a.W;
+    const X6Group& G = a.g[x6_group_of(a, tile)];
+    const int mt = (tile - G.t0) % nM;
+    const int pt = (tile - G.t0) / nM;
+    const int HW = G.H * G.W;
     // thread -> (quad of channels, pixel); pixels fastest so slab reads stay coalesced
     const int e = blockIdx.y * 256 + threadIdx.x;  // < MT/4 * PT
     const int pl = e % PT, mq = e / PT;
     const int ml0 = mq * 4;
     const int mg = mt * MT + ml0;  // first channel of the quad
     const int p = pt * PT + pl;
-    if (p >= a.npix) return;
+    if (p >= G.npix) return;
     const int cout8 = (G.cout + 7) & ~7;
     if (mg >= (G.out_f32 ? G.cout : cout8)) return;
     float v[4];
@@ -499,7 +502,7 @@ __global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
         return;
     }
     const int grp = mg >> 3, half = (mg >> 2) & 1;
-    const int y = rem / a.W, x = rem - y * a.W;
+    const int y = rem / G.W, x = rem - y * G.W;
     store4_x6(static_cast<uint8_t*>(G.out) + (size_t)x6_unit(G.out_l, n, grp, y, x) * 16 + half * 8, G.out_ps, v);
     if (G.out2)
         store4_x6(static_cast<uint8_t*>(G.out2) + (size_t)x6_unit(G.out2_l, n, grp, y, x) * 16 + half * 8, G.out2_ps,
@@ -709,8 +712,23 @@ void x6_pack_weights(const float* w, int cout, int cin, int ks, int Mpad, int* n
         }
 }
 
+// number the groups' tiles (X6Group::t0, X6Args::tiles) for an MT x PT tile
+X6Args x6_number_tiles(const X6Args& a0, int mt, int pt) {
+    X6Args a = a0;
+    if (a.ngroups < 1 || a.ngroups > kX6Groups || a.Mpad % mt) throw std::invalid_argument("conv_x6: bad groups");
+    int t = 0;
+    for (int g = 0; g < a.ngroups; ++g) {
+        if (a.g[g].npix <= 0) throw std::invalid_argument("conv_x6: empty group");
+        a.g[g].t0 = t;
+        t += (a.Mpad / mt) * ((a.g[g].npix + pt - 1) / pt);
+    }
+    a.tiles = t;
+    return a;
+}
+
 template <int MT, int PT>
-static void launch_x6_tile(const X6Args& a, hipStream_t st) {
+static void launch_x6_tile(const X6Args& a0, hipStream_t st) {
+    const X6Args a = x6_number_tiles(a0, MT, PT);
     const dim3 blk(64 * x6_waves(MT, PT));
     if (a.small != 0)
         hipLaunchKernelGGL((conv_x6<MT, PT, true, 0>), dim3(a.sk_grid), blk, 0, st, a);
@@ -722,9 +740,13 @@ static void launch_x6_tile(const X6Args& a, hipStream_t st) {
         hipLaunchKernelGGL((conv_x6<MT, PT, false, 1>), dim3(a.sk_grid), blk, 0, st, a);
     else
         hipLaunchKernelGGL((conv_x6<MT, PT, false, 0>), dim3(a.sk_grid), blk, 0, st, a);
-    const int tiles = (a.Mpad / MT) * ((a.npix + PT - 1) / PT) * a.ngroups;
-    if (a.sk_grid != tiles)
-        hipLaunchKernelGGL((conv_x6_fixup<MT, PT>), dim3(tiles, MT * PT / 4 / 256), dim3(256), 0, st, a);
+    if (a.sk_grid != a.tiles)
+        hipLaunchKernelGGL((conv_x6_fixup<MT, PT>), dim3(a.tiles, MT * PT / 4 / 256), dim3(256), 0, st, a);
+}
+
+void launch_conv_x6_fixup(const X6Args& a, int mt, int pt, hipStream_t st) {
+    if (mt != 128 || pt != 256) throw std::invalid_argument("conv_x6_fixup: tile");
+    hipLaunchKernelGGL((conv_x6_fixup<128, 256>), dim3(a.tiles, 128 * 256 / 4 / 256), dim3(256), 0, st, a);
 }
 
 void launch_conv_x6(const X6Args& a, int mt, int pt, hipStream_t st) {

@@ -209,6 +209,12 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_CONV7_WIN");
         return !(e && e[0] == '0');
     }();
+    // OPOSE_WIN_SK=0: conv_win_x6 only on data-parallel grids that fill the chip (no stream-K
+    // window launches; the A/B of the planner's window pricing)
+    bool win_dp_only = [] {
+        const char* e = getenv("OPOSE_WIN_SK");
+        return e && e[0] == '0';
+    }();
     // conv1_2 + pool by conv3_pool_win_x6 (input window in LDS; OPOSE_CONV12_WIN=0: conv_x6's
     // pooled 64 x 128 tile over the im2col stream)
     bool win12 = [] {
@@ -230,6 +236,15 @@ struct opose_ctx {
     bool scale_streams = [] {
         const char* e = getenv("OPOSE_SCALE_STREAMS");
         return !(e && e[0] == '0');
+    }();
+    // split-bf16 path: the scales' networks in lockstep, one conv launch per layer for all of them
+    // (Hand: default; OPOSE_LOCKSTEP=0: one network per scale, concurrent streams when
+    // scale_streams).  Body pyramids: OPOSE_LOCKSTEP=2 -- by default they keep one network per
+    // scale, so that the scale-sharded C5 split (opose_body_scale_maps per rank) reproduces
+    // Body(frame) bit for bit: a lockstep launch's stream-K plan depends on every scale.
+    int lockstep = [] {
+        const char* e = getenv("OPOSE_LOCKSTEP");
+        return e ? std::atoi(e) : 1;
     }();
     hipStream_t sstream[kMaxScales] = {};
     hipEvent_t ev_fork = nullptr, ev_join[kMaxScales] = {};
@@ -343,7 +358,10 @@ struct TileChoice {
 // holds k >= 2 co-resident workgroups finishes them in k * work; a lone workgroup (one wave per
 // SIMD) runs at ~60 %.  Stream-K (grid = all resident slots) balances the chip exactly and
 // pays for the partial slabs of tiles it splits plus one fixup launch.
-TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false, bool dp_only = false) {
+TileChoice choose_tile(int Mpad, const std::vector<int>& gpix, int nK, bool x6 = false, bool dp_only = false,
+                       double* cost_out = nullptr) {
+    long npix_all = 0;
+    for (int n : gpix) npix_all += n;
     static const int cfg[6][3] = {{128, 128, 2}, {128, 256, 1}, {256, 128, 1},
                                   {128, 64, 3},  {64, 128, 3},  {64, 64, 4}};  // mt, pt, WG/CU
     // split-bf16 kernel: 2.5x the MFMA rate per chunk, more LDS per workgroup
@@ -358,7 +376,7 @@ TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false,
     // Hand() 10.0 -> 9.9 ms, C5 and the bench unchanged; the same weights on the bench's
     // 32-frame layers cost 6 % (scripts/c2_tile_ab.sh)
     static const double ovh6_small[6] = {1.0, 1.0, 0.96, 1.1, 1.1, 1.6};
-    const double* ovh6 = (long)npix * ngroups <= 16384 ? ovh6_small : ovh6_big;
+    const double* ovh6 = npix_all <= 16384 ? ovh6_small : ovh6_big;
     const double rate = x6 ? 0.4 : 1.0;
     // relative cost per MFMA of the smaller tiles of the fp32 kernel (more load/issue work per
     // MFMA), measured with scripts/conv_timing.py
@@ -368,7 +386,8 @@ TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false,
     for (int c = 0; c < 6; ++c) {
         const int mt = cfg[c][0], pt = cfg[c][1], occ = x6 ? occ6[c] : cfg[c][2];
         if (Mpad % mt) continue;
-        const long tiles = (long)(Mpad / mt) * ((npix + pt - 1) / pt) * ngroups;
+        long tiles = 0;
+        for (int n : gpix) tiles += (long)(Mpad / mt) * ((n + pt - 1) / pt);
         const double unit = (mt / 64.0) * (pt / 64.0) * (x6 ? ovh6[c] : ovh[c]) * rate;
         // data parallel
         const long per_cu = (tiles + 255) / 256;
@@ -402,6 +421,34 @@ TileChoice choose_tile(int Mpad, int npix, int ngroups, int nK, bool x6 = false,
             }
         }
     }
+    if (cost_out) *cost_out = best_cost;
+    return best;
+}
+
+// conv_win_x6 (128 x 256 tiles, input window in LDS) priced in choose_tile's units: data parallel
+// when its rounds fill the chip, else stream-K over 256 workgroups.  `eff`: its cost per chunk
+// relative to conv_x6's 128 x 256 tile (fewer DMA instructions and LDS-DMA bytes).
+TileChoice choose_win(int Mpad, const std::vector<int>& gpix, int nK, double eff, double* cost_out) {
+    long tiles = 0;
+    for (int n : gpix) tiles += (long)(Mpad / 128) * ((n + 255) / 256);
+    const double unit = 8.0 * 0.4 * eff;
+    const long per_cu = (tiles + 255) / 256;
+    double best_cost = (double)per_cu * nK * unit;
+    TileChoice best{128, 256, (int)tiles};
+    const long iters = tiles * nK;
+    const long grid = std::min<long>(256, iters / 8);
+    if (grid >= 1 && grid != tiles) {
+        const double per_wg = (double)iters / grid;
+        const long segs = grid > 2 * tiles ? grid + tiles : std::min<long>(tiles, 2 * grid);
+        const double slab_bytes = grid > 2 * tiles ? (double)segs * 128 * 256 * 4.0 * 2.0 + (double)tiles * 128 * 256 * 4.0
+                                                   : (double)segs * 128 * 256 * 4.0 * 3.0;
+        const double sk = per_wg * unit + slab_bytes / 5e12 / 0.42e-6 + 8.0;
+        if (sk < best_cost * 0.97) {
+            best_cost = sk;
+            best = {128, 256, (int)grid};
+        }
+    }
+    *cost_out = best_cost;
     return best;
 }
 
@@ -534,7 +581,7 @@ static void run_conv(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W
     for (int g = 0; g < ng; ++g)  // the im2col gather addresses the input with 32-bit byte offsets
         if ((double)N * ins[g].cstride * H * W * 4.0 >= 2147483648.0)
             throw std::invalid_argument("activation slab >= 2 GiB: split the batch");
-    const TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.Kpad / 32);
+    const TileChoice t = choose_tile(a.Mpad, std::vector<int>(ng, a.npix), a.Kpad / 32);
     a.ngroups = ng;
     a.sk_grid = t.grid;
     a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
@@ -632,87 +679,124 @@ static XAct x6pact(uint8_t* p, int cg, int goff, int N, int H, int W) {
     return a;
 }
 
-// pool: MaxPool2d(2, 2) (src/model.py:10-13, floor mode) fused into the epilogue; out0 is then the
+// One GEMM of a conv launch (an X6Group): a scale's frames through one branch's weights.
+struct ConvSeg {
+    DevConv* c;
+    int N, H, W;
+    XAct in, out, dup;  // dup: optional duplicate X6 destination
+    bool relu;
+};
+
+// Run convs of one shape (ks, Cin, Mpad) over up to kX6Groups segments per launch: the CPM
+// branch pair of a stage and the scales of a pyramid share one grid (X6Args groups).
+// pool: MaxPool2d(2, 2) (src/model.py:10-13, floor mode) fused into the epilogue; out is then the
 // pooled [N][(H/2)(W/2)] X6 tensor (conv outputs the floor mode drops are never computed)
-static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W, XAct in0, XAct out0, XAct in1,
-                        XAct out1, bool relu0, bool relu1, XAct dup = XAct{}, bool pool = false) {
+static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, bool pool = false) {
+    if (segs.empty()) return;
+    if (segs.size() > (size_t)kX6Groups) {  // more scales x branches than one launch holds
+        for (size_t i = 0; i < segs.size(); i += kX6Groups)
+            run_conv_x6_segs(h, std::vector<ConvSeg>(segs.begin() + i, segs.begin() + std::min(segs.size(), i + kX6Groups)),
+                             pool);
+        return;
+    }
+    DevConv* c0 = segs[0].c;
     X6Args a{};
-    const int ng = c1 ? 2 : 1;
-    a.N = N;
-    a.H = H;
-    a.W = W;
+    const int ng = (int)segs.size();
     a.ks = c0->ks;
     a.pad = c0->pad;
     a.cin_g = c0->cin_g;
     a.small = c0->small6 ? 1 : 0;
     a.nK = c0->nK6;
     a.Mpad = c0->Mpad;
-    a.npix = pool ? N * (H / 2) * (W / 2) * 4 : N * H * W;
     a.pool = pool ? 1 : 0;
-    if (pool && (c1 || dup.p || out0.f32)) throw std::invalid_argument("pooled conv: single X6 output only");
-    DevConv* cs[2] = {c0, c1};
-    XAct ins[2] = {in0, in1}, outs[2] = {out0, out1};
-    bool relus[2] = {relu0, relu1};
+    a.ngroups = ng;
+    std::vector<int> gpix;
+    bool win_ok = h->win7 && !pool;
+    double flops = 0;
+    long npix_all = 0;
     for (int g = 0; g < ng; ++g) {
+        const ConvSeg& sg = segs[g];
+        DevConv* c = sg.c;
+        if (c->ks != c0->ks || c->cin_g != c0->cin_g || c->Mpad != c0->Mpad || c->nK6 != c0->nK6)
+            throw std::invalid_argument("conv segments of different shapes");
+        if (pool && (sg.dup.p || sg.out.f32)) throw std::invalid_argument("pooled conv: single X6 output only");
         X6Group& G = a.g[g];
-        G.in = static_cast<const uint8_t*>(ins[g].p);
-        G.in_ps = ins[g].ps;
-        G.in_l = ins[g].l;
-        G.wt = cs[g]->wx6;
-        G.bias = cs[g]->bias;
-        G.out = outs[g].p;
-        G.out_ps = outs[g].ps;
-        G.out_l = outs[g].l;
-        G.out_c = outs[g].c;
-        G.out_off = outs[g].off;
-        G.out_f32 = outs[g].f32 ? 1 : 0;
-        G.out2 = nullptr;
-        G.cout = cs[g]->cout;
-        G.relu = relus[g] ? 1 : 0;
-    }
-    if (dup.p) {
-        a.g[0].out2 = dup.p;
-        a.g[0].out2_ps = dup.ps;
-        a.g[0].out2_l = dup.l;
-    }
-    if (ng == 1) a.g[1] = a.g[0];
-    // batched 3x3 / 7x7 layers on padded inputs: the LDS-window kernel over whole 128 x 256
-    // tiles, when the data-parallel grid fills the chip's 256 CUs in its rounds (>= 85 %: 236,
-    // 472 and 944 tiles on the bench; a hand crop's 266 tiles would leave the second round
-    // nearly empty -- conv_x6 balances such layers by stream-K)
-    const long win_tiles = (long)(a.Mpad / 128) * ((a.npix + 255) / 256) * ng;
-    const double win_fill = (double)win_tiles / (double)(((win_tiles + 255) / 256) * 256);
-    if (h->win7 && c0->wx6p && (!c1 || c1->wx6p) && !pool && in0.padded && (!c1 || in1.padded) &&
-        win_tiles >= 192 && win_fill >= 0.85 && conv_win_fits(N, H, W, c0->ks)) {
-        a.ngroups = ng;
-        a.nK = c0->nK6p;
-        a.g[0].wt = c0->wx6p;
-        a.g[1].wt = (c1 ? c1 : c0)->wx6p;
-        a.sk_grid = (int)win_tiles;
-        double flops = 0;
-        for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)c0->K * a.npix;
-        ProfEntry pe;
-        h->prof_begin(pe, conv_class(c0->ks), flops, 0);
-        if (h->detail) pe.detail = "layer/" + c0->name + "/win/s" + std::to_string(win_tiles) + "/n" + std::to_string(a.npix);
-        launch_conv_win_x6(a, h->stream);
-        h->prof_end(pe);
-        return;
+        G.in = static_cast<const uint8_t*>(sg.in.p);
+        G.in_ps = sg.in.ps;
+        G.in_l = sg.in.l;
+        G.wt = c->wx6;
+        G.bias = c->bias;
+        G.out = sg.out.p;
+        G.out_ps = sg.out.ps;
+        G.out_l = sg.out.l;
+        G.out_c = sg.out.c;
+        G.out_off = sg.out.off;
+        G.out_f32 = sg.out.f32 ? 1 : 0;
+        G.out2 = sg.dup.p;
+        G.out2_ps = sg.dup.ps;
+        G.out2_l = sg.dup.l;
+        G.cout = c->cout;
+        G.relu = sg.relu ? 1 : 0;
+        G.N = sg.N;
+        G.H = sg.H;
+        G.W = sg.W;
+        G.npix = pool ? sg.N * (sg.H / 2) * (sg.W / 2) * 4 : sg.N * sg.H * sg.W;
+        gpix.push_back(G.npix);
+        npix_all += G.npix;
+        flops += 2.0 * c->cout * (double)c->K * (pool ? 4.0 * sg.N * (sg.H / 2) * (sg.W / 2) : (double)G.npix);
+        win_ok = win_ok && c->wx6p && sg.in.padded && conv_win_fits(sg.N, sg.H, sg.W, c->ks);
     }
     // pooled convs run whole tiles (data parallel): price only those
-    TileChoice t = choose_tile(a.Mpad, a.npix, ng, a.nK, true, pool);
-    if (pool) t.grid = (a.Mpad / t.mt) * ((a.npix + t.pt - 1) / t.pt) * ng;
-    a.ngroups = ng;
+    double cost = 0;
+    TileChoice t = choose_tile(a.Mpad, gpix, a.nK, true, pool, &cost);
+    if (pool) t.grid = x6_number_tiles(a, t.mt, t.pt).tiles;
+    // 3x3 / 7x7 layers on padded inputs: the LDS-window kernel when it prices lower (its chunk
+    // costs ~0.8 of conv_x6's at 7x7 -- 290 vs 262 TF/s on the bench's 236-tile grids, 225 vs
+    // 200 TF/s stream-K on a hand crop's pyramid -- and ~0.95 at 3x3)
+    std::string kind = "x6";
+    if (win_ok && !h->win_dp_only) {
+        double wcost = 0;
+        const TileChoice tw = choose_win(a.Mpad, gpix, c0->nK6p, c0->ks == 7 ? 0.8 : 0.95, &wcost);
+        if (wcost < cost) {
+            t = tw;
+            kind = "win";
+        }
+    } else if (win_ok) {  // OPOSE_WIN_SK=0: the window kernel only on data-parallel grids that fill the chip
+        long tiles = 0;
+        for (int n : gpix) tiles += (long)(a.Mpad / 128) * ((n + 255) / 256);
+        const double fill = (double)tiles / (double)(((tiles + 255) / 256) * 256);
+        if (tiles >= 192 && fill >= 0.85) {
+            t = TileChoice{128, 256, (int)tiles};
+            kind = "win";
+        }
+    }
     a.sk_grid = t.grid;
     a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
-    double flops = 0;
-    for (int g = 0; g < ng; ++g) flops += 2.0 * cs[g]->cout * (double)c0->K * a.npix;
     ProfEntry pe;
     h->prof_begin(pe, conv_class(c0->ks), flops, 0);
-    if (h->detail)
-        pe.detail = "layer/" + c0->name + "/x6/" + std::to_string(t.mt) + "x" + std::to_string(t.pt) + "s" +
-                    std::to_string(t.grid) + "/n" + std::to_string(a.npix);
-    launch_conv_x6(a, t.mt, t.pt, h->stream);
+    if (h->detail) {
+        std::string nm = c0->name;
+        for (int g = 1; g < ng; ++g)
+            if (segs[g].c != c0 && nm.find(segs[g].c->name) == std::string::npos) nm += "|" + segs[g].c->name;
+        pe.detail = "layer/" + nm + "/" + kind + "/" + std::to_string(t.mt) + "x" + std::to_string(t.pt) + "s" +
+                    std::to_string(t.grid) + "/g" + std::to_string(ng) + "/n" + std::to_string(npix_all);
+    }
+    if (kind == "win") {
+        a.nK = c0->nK6p;
+        for (int g = 0; g < ng; ++g) a.g[g].wt = segs[g].c->wx6p;
+        launch_conv_win_x6(a, h->stream);
+    } else {
+        launch_conv_x6(a, t.mt, t.pt, h->stream);
+    }
     h->prof_end(pe);
+}
+
+// the single-geometry form: one conv (c1 null) or a CPM branch pair on N x H x W
+static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W, XAct in0, XAct out0, XAct in1,
+                        XAct out1, bool relu0, bool relu1, XAct dup = XAct{}, bool pool = false) {
+    std::vector<ConvSeg> segs{ConvSeg{c0, N, H, W, in0, out0, dup, relu0}};
+    if (c1) segs.push_back(ConvSeg{c1, N, H, W, in1, out1, XAct{}, relu1});
+    run_conv_x6_segs(h, segs, pool);
 }
 
 // Zero the padding units of X6P buffers (cg groups each) for an N x H x W geometry.  The convs
@@ -753,19 +837,25 @@ static void clear_x6p_pads(opose_ctx* h, std::initializer_list<std::pair<DevBuf*
     g_alloc_epoch.fetch_add(1);
 }
 
-// VGG trunk on X6 activations: x fp32 [N,3,H,W] -> final trunk conv written via `last` (+ dup).
-// Full and half resolution run on dense X6 buffers (A / B); from the second pool on (H/4: conv3_x,
-// H/8: conv4_x, conv5_x of the hand) the activations are padded X6P (P0 / P1, Q0 / Q1), which the
-// windowed conv_win_x6 reads (conv_x6 reads either layout).
-static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, int W, XAct last, XAct dup) {
+// One scale of a network forward.  The scales of a pyramid (Hand()'s four, C5's) run in lockstep:
+// layer by layer, one conv launch covers every scale (X6 groups with their own geometry), so a
+// single crop's small layers share one grid instead of each filling a fraction of the chip.
+struct NetSeg {
+    const float* x;  // [N][3][Hp][Wp] fp32 network input
+    int N, Hp, Wp;
+    int slot;  // workspace set (opose_ctx::ws)
+};
+
+// VGG trunk on X6 activations: every segment's x -> its final trunk conv written via last[i]
+// (+ dup[i]).  Full and half resolution run on dense X6 buffers (A / B); from the second pool on
+// (H/4: conv3_x, H/8: conv4_x, conv5_x of the hand) the activations are padded X6P (P0 / P1,
+// Q0 / Q1), which the windowed conv_win_x6 reads (conv_x6 reads either layout).
+static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs, const std::vector<XAct>& last,
+                         const std::vector<XAct>& dup) {
     const std::vector<Spec> vgg = net == OPOSE_NET_BODY ? vgg_body() : vgg_hand();
-    const size_t npix = (size_t)N * H * W;
-    const size_t act = npix * 8 * 16 * 3;  // 64 channels at full resolution = the largest dense tensor
-    uint8_t* A = h->w().x6A.ensure<uint8_t>(act, h->stream);
-    uint8_t* B = h->w().x6B.ensure<uint8_t>(act, h->stream);
+    const size_t ns = segs.size();
     // padded levels (fused pooling only: the separate maxpool_x6 reads and writes dense X6)
     const bool padded = h->fused_pool;
-    const int H4 = H / 4, W4 = W / 4, H8 = H / 8, W8 = W / 8;
     int maxg4 = 0, maxg8 = 0;  // widest activation (groups) at H/4 and H/8
     {
         int lvl = 0;
@@ -778,182 +868,284 @@ static void run_trunk_x6(opose_ctx* h, int net, const float* x, int N, int H, in
             lvl = out_lvl;
         }
     }
-    uint8_t *P0 = nullptr, *P1 = nullptr, *Q0 = nullptr, *Q1 = nullptr;
-    if (padded) {
-        P0 = h->w().x6P0.ensure<uint8_t>(x6p_plane(N, H4, W4) * maxg4 * 48, h->stream);
-        P1 = h->w().x6P1.ensure<uint8_t>(x6p_plane(N, H4, W4) * maxg4 * 48, h->stream);
-        Q0 = h->w().x6Q0.ensure<uint8_t>(x6p_plane(N, H8, W8) * maxg8 * 48, h->stream);
-        Q1 = h->w().x6Q1.ensure<uint8_t>(x6p_plane(N, H8, W8) * maxg8 * 48, h->stream);
-        clear_x6p_pads(h, {{&h->w().x6P0, maxg4}, {&h->w().x6P1, maxg4}}, N, H4, W4);
-        clear_x6p_pads(h, {{&h->w().x6Q0, maxg8}, {&h->w().x6Q1, maxg8}}, N, H8, W8);
+    struct Bufs {
+        uint8_t *A, *B, *P0, *P1, *Q0, *Q1;
+        XAct cur;
+    };
+    std::vector<Bufs> bs(ns);
+    for (size_t i = 0; i < ns; ++i) {
+        const NetSeg& sg = segs[i];
+        auto& w = h->ws[sg.slot];
+        const int N = sg.N, H = sg.Hp, W = sg.Wp;
+        const size_t act = (size_t)N * H * W * 8 * 16 * 3;  // 64 channels at full resolution: the largest dense tensor
+        Bufs& b = bs[i];
+        b.A = w.x6A.ensure<uint8_t>(act, h->stream);
+        b.B = w.x6B.ensure<uint8_t>(act, h->stream);
+        b.P0 = b.P1 = b.Q0 = b.Q1 = nullptr;
+        if (padded) {
+            const int H4 = H / 4, W4 = W / 4, H8 = H / 8, W8 = W / 8;
+            b.P0 = w.x6P0.ensure<uint8_t>(x6p_plane(N, H4, W4) * maxg4 * 48, h->stream);
+            b.P1 = w.x6P1.ensure<uint8_t>(x6p_plane(N, H4, W4) * maxg4 * 48, h->stream);
+            b.Q0 = w.x6Q0.ensure<uint8_t>(x6p_plane(N, H8, W8) * maxg8 * 48, h->stream);
+            b.Q1 = w.x6Q1.ensure<uint8_t>(x6p_plane(N, H8, W8) * maxg8 * 48, h->stream);
+            clear_x6p_pads(h, {{&w.x6P0, maxg4}, {&w.x6P1, maxg4}}, N, H4, W4);
+            clear_x6p_pads(h, {{&w.x6Q0, maxg8}, {&w.x6Q1, maxg8}}, N, H8, W8);
+        }
     }
-    // output buffer for a layer at resolution level `lvl` (0: H, 1: H/2, 2: H/4, 3: H/8), not `avoid`
-    auto out_buf = [&](int lvl, int og, const void* avoid) -> XAct {
-        const int hh = H >> lvl, ww = W >> lvl;
-        if (!padded || lvl < 2) return x6act(avoid == A ? B : A, og, 0, N, hh, ww);
-        uint8_t* p = lvl == 2 ? (avoid == P0 ? P1 : P0) : (avoid == Q0 ? Q1 : Q0);
+    // output buffer of segment i for a layer at resolution level `lvl` (0: H, 1: H/2, 2: H/4,
+    // 3: H/8), not the one its input is in
+    auto out_buf = [&](size_t i, int lvl, int og) -> XAct {
+        const Bufs& b = bs[i];
+        const void* avoid = b.cur.p;
+        const int N = segs[i].N, hh = segs[i].Hp >> lvl, ww = segs[i].Wp >> lvl;
+        if (!padded || lvl < 2) return x6act(avoid == b.A ? b.B : b.A, og, 0, N, hh, ww);
+        uint8_t* p = lvl == 2 ? (avoid == b.P0 ? b.P1 : b.P0) : (avoid == b.Q0 ? b.Q1 : b.Q0);
         return x6pact(p, og, 0, N, hh, ww);
     };
-    XAct cur;
     int lvl = 0;
-    for (size_t i = 0; i < vgg.size(); ++i) {
-        const Spec& s = vgg[i];
+    for (size_t li = 0; li < vgg.size(); ++li) {
+        const Spec& s = vgg[li];
         DevConv* c = find_conv(h, net, s.name);
-        const int hh = H >> lvl, ww = W >> lvl;
-        if (i == 0 && s.cin == 3 && s.cout == 64 && s.ks == 3 && s.pad == 1 && vgg.size() > 1 && h->first_direct) {
+        if (li == 0 && s.cin == 3 && s.cout == 64 && s.ks == 3 && s.pad == 1 && vgg.size() > 1 && h->first_direct) {
             // conv1_1 straight from the fp32 input (conv_first_x6), no input split
-            ProfEntry pe;
-            h->prof_begin(pe, "conv3x3", 2.0 * 64 * 27 * (double)npix, 0);
-            if (h->detail) pe.detail = "layer/" + s.name + "/first_direct/n" + std::to_string(npix);
-            launch_conv_first_x6(x, N, 3, H, W, c->wt, c->Mpad, c->bias, A, (uint32_t)(npix * 8 * 16), h->stream);
-            h->prof_end(pe);
-            cur = x6act(A, 8, 0, N, H, W);
+            for (size_t i = 0; i < ns; ++i) {
+                const NetSeg& sg = segs[i];
+                const size_t npix = (size_t)sg.N * sg.Hp * sg.Wp;
+                ProfEntry pe;
+                h->prof_begin(pe, "conv3x3", 2.0 * 64 * 27 * (double)npix, 0);
+                if (h->detail) pe.detail = "layer/" + s.name + "/first_direct/n" + std::to_string(npix);
+                launch_conv_first_x6(sg.x, sg.N, 3, sg.Hp, sg.Wp, c->wt, c->Mpad, c->bias, bs[i].A,
+                                     (uint32_t)(npix * 8 * 16), h->stream);
+                h->prof_end(pe);
+                bs[i].cur = x6act(bs[i].A, 8, 0, sg.N, sg.Hp, sg.Wp);
+            }
             continue;
         }
-        if (i == 0) {
-            uint8_t* X = h->w().x6in.ensure<uint8_t>(npix * 16 * 3, h->stream);
-            ProfEntry pe;
-            h->prof_begin(pe, "to_x6", 0, (double)npix * (12 + 48));
-            launch_to_x6(x, 3, 0, 3, N, H * W, X, 1, 0, (uint32_t)(npix * 16), h->stream);
-            h->prof_end(pe);
-            cur = x6act(X, 1, 0, N, H, W);
+        if (li == 0) {
+            for (size_t i = 0; i < ns; ++i) {
+                const NetSeg& sg = segs[i];
+                const size_t npix = (size_t)sg.N * sg.Hp * sg.Wp;
+                uint8_t* X = h->ws[sg.slot].x6in.ensure<uint8_t>(npix * 16 * 3, h->stream);
+                ProfEntry pe;
+                h->prof_begin(pe, "to_x6", 0, (double)npix * (12 + 48));
+                launch_to_x6(sg.x, 3, 0, 3, sg.N, sg.Hp * sg.Wp, X, 1, 0, (uint32_t)(npix * 16), h->stream);
+                h->prof_end(pe);
+                bs[i].cur = x6act(X, 1, 0, sg.N, sg.Hp, sg.Wp);
+            }
         }
-        const bool final_layer = i + 1 == vgg.size();
+        const bool final_layer = li + 1 == vgg.size();
         const int og = (s.cout + 7) / 8;
         const bool pooled = s.name == "conv1_2" || s.name == "conv2_2" || s.name == "conv3_4";
-        if (pooled && h->fused_pool && h->win12 && s.name == "conv1_2" && !cur.padded && cur.l.fs == 8u * hh * ww &&
-            c->cin == 64 && c->cout == 64 && c->ks == 3 && c->pad == 1 && c->Mpad == 64 && c->nK6 == 18 &&
-            !c->small6) {
+        if (pooled && h->fused_pool && h->win12 && s.name == "conv1_2" && c->cin == 64 && c->cout == 64 && c->ks == 3 &&
+            c->pad == 1 && c->Mpad == 64 && c->nK6 == 18 && !c->small6) {
             // conv1_2 + pool with the input window in LDS instead of the 9-tap im2col stream
-            const size_t np = (size_t)N * hh * ww, npo = (size_t)N * (hh / 2) * (ww / 2);
-            const XAct out = out_buf(lvl + 1, og, cur.p);
-            ProfEntry pe;
-            h->prof_begin(pe, "conv3x3", 2.0 * 64 * 576 * (double)(npo * 4), 0);
-            if (h->detail) pe.detail = "layer/" + s.name + "/x6win/n" + std::to_string(npo * 4);
-            launch_conv3_pool_win_x6(static_cast<const uint8_t*>(cur.p), (uint32_t)(np * 8 * 16), N, hh, ww, c->wx6,
-                                     c->bias, static_cast<uint8_t*>(out.p), (uint32_t)(npo * 8 * 16), h->stream);
-            h->prof_end(pe);
-            cur = out;
+            for (size_t i = 0; i < ns; ++i) {
+                const NetSeg& sg = segs[i];
+                const int hh = sg.Hp >> lvl, ww = sg.Wp >> lvl;
+                if (bs[i].cur.padded || bs[i].cur.l.fs != 8u * hh * ww) throw std::logic_error("conv1_2 input layout");
+                const size_t np = (size_t)sg.N * hh * ww, npo = (size_t)sg.N * (hh / 2) * (ww / 2);
+                const XAct out = out_buf(i, lvl + 1, og);
+                ProfEntry pe;
+                h->prof_begin(pe, "conv3x3", 2.0 * 64 * 576 * (double)(npo * 4), 0);
+                if (h->detail) pe.detail = "layer/" + s.name + "/x6win/n" + std::to_string(npo * 4);
+                launch_conv3_pool_win_x6(static_cast<const uint8_t*>(bs[i].cur.p), (uint32_t)(np * 8 * 16), sg.N, hh,
+                                         ww, c->wx6, c->bias, static_cast<uint8_t*>(out.p), (uint32_t)(npo * 8 * 16),
+                                         h->stream);
+                h->prof_end(pe);
+                bs[i].cur = out;
+            }
             ++lvl;
             continue;
         }
-        if (pooled && h->fused_pool) {  // conv + MaxPool2d(2, 2) in one launch
-            const XAct out = out_buf(lvl + 1, og, cur.p);
-            run_conv_x6(h, c, nullptr, N, hh, ww, cur, out, XAct{}, XAct{}, true, false, XAct{}, true);
-            cur = out;
+        std::vector<ConvSeg> cs;
+        std::vector<XAct> outs;
+        const bool fuse = pooled && h->fused_pool;  // conv + MaxPool2d(2, 2) in one launch
+        for (size_t i = 0; i < ns; ++i) {
+            const NetSeg& sg = segs[i];
+            const XAct out = fuse ? out_buf(i, lvl + 1, og) : final_layer ? last[i] : out_buf(i, lvl, og);
+            outs.push_back(out);
+            cs.push_back(ConvSeg{c, sg.N, sg.Hp >> lvl, sg.Wp >> lvl, bs[i].cur, out,
+                                 final_layer && !fuse ? dup[i] : XAct{}, true});
+        }
+        run_conv_x6_segs(h, cs, fuse);
+        for (size_t i = 0; i < ns; ++i) bs[i].cur = outs[i];
+        if (fuse) {
             ++lvl;
             continue;
         }
-        const XAct out = final_layer ? last : out_buf(lvl, og, cur.p);
-        run_conv_x6(h, c, nullptr, N, hh, ww, cur, out, XAct{}, XAct{}, true, false, final_layer ? dup : XAct{});
-        cur = out;
         if (pooled) {  // separate MaxPool2d(2, 2) (fused_pool off: dense buffers throughout)
-            const size_t np = (size_t)N * hh * ww;
-            const XAct pd = x6act(cur.p == A ? B : A, og, 0, N, hh / 2, ww / 2);
-            ProfEntry pe;
-            h->prof_begin(pe, "maxpool", 0, (double)np * og * 48 * 1.25);
-            launch_maxpool_x6(static_cast<const uint8_t*>(cur.p), (uint32_t)(np * og * 16), static_cast<uint8_t*>(pd.p),
-                              (uint32_t)((size_t)N * (hh / 2) * (ww / 2) * og * 16), N * og, hh, ww, h->stream);
-            h->prof_end(pe);
-            cur = pd;
+            for (size_t i = 0; i < ns; ++i) {
+                const NetSeg& sg = segs[i];
+                const int hh = sg.Hp >> lvl, ww = sg.Wp >> lvl;
+                const size_t np = (size_t)sg.N * hh * ww;
+                Bufs& b = bs[i];
+                const XAct pd = x6act(b.cur.p == b.A ? b.B : b.A, og, 0, sg.N, hh / 2, ww / 2);
+                ProfEntry pe;
+                h->prof_begin(pe, "maxpool", 0, (double)np * og * 48 * 1.25);
+                launch_maxpool_x6(static_cast<const uint8_t*>(b.cur.p), (uint32_t)(np * og * 16),
+                                  static_cast<uint8_t*>(pd.p), (uint32_t)((size_t)sg.N * (hh / 2) * (ww / 2) * og * 16),
+                                  sg.N * og, hh, ww, h->stream);
+                h->prof_end(pe);
+                b.cur = pd;
+            }
             ++lvl;
         }
     }
 }
 
-// bodypose_model.forward on X6 activations; output fp32 in S0 with the fp32 path's layout
-// (channel stride 185: paf [0,38), heat [38,57))
-static float* body_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
-    const int hl = Hp / 8, wl = Wp / 8;
-    const size_t px = (size_t)N * hl * wl;
+// bodypose_model.forward on X6 activations, every segment in lockstep; per segment the fp32
+// output in its slot's S0 with the fp32 path's layout (channel stride 185: paf [0,38), heat [38,57))
+static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& segs) {
     const int SG = 24, TG = 32, UG = 128;  // [L1 | L2 | trunk] = 5 + 3 + 16 groups; 256 / 1024 channels
-    // S (stage inputs) and T (branch activations): padded X6P, read by the 7x7 / 3x3 convs
-    const size_t plane = x6p_plane(N, hl, wl);
-    uint8_t* S[2] = {h->w().x6S0.ensure<uint8_t>(plane * SG * 48, h->stream),
-                     h->w().x6S1.ensure<uint8_t>(plane * SG * 48, h->stream)};
-    uint8_t* T[2] = {h->w().x6T0.ensure<uint8_t>(plane * TG * 48, h->stream),
-                     h->w().x6T1.ensure<uint8_t>(plane * TG * 48, h->stream)};
-    uint8_t* U = h->w().x6U.ensure<uint8_t>(px * UG * 48, h->stream);
-    float* O = h->w().S0.ensure<float>(px * 185, h->stream);
-    clear_x6p_pads(h, {{&h->w().x6S0, SG}, {&h->w().x6S1, SG}, {&h->w().x6T0, TG}, {&h->w().x6T1, TG}}, N, hl, wl);
     const int net = OPOSE_NET_BODY;
-    auto s_ = [&](int i, int goff) { return x6pact(S[i], SG, goff, N, hl, wl); };
-    auto t_ = [&](int i, int goff) { return x6pact(T[i], TG, goff, N, hl, wl); };
-    auto u_ = [&](int goff) { return x6act(U, UG, goff, N, hl, wl); };
-    run_trunk_x6(h, net, x, N, Hp, Wp, s_(0, 8), s_(1, 8));
-    run_conv_x6(h, find_conv(h, net, "conv5_1_CPM_L1+L2"), nullptr, N, hl, wl, s_(0, 8), t_(0, 0), XAct{}, XAct{},
-                true, false);
-    run_conv_x6(h, find_conv(h, net, "conv5_2_CPM_L1"), find_conv(h, net, "conv5_2_CPM_L2"), N, hl, wl, t_(0, 0),
-                t_(1, 0), t_(0, 16), t_(1, 16), true, true);
-    run_conv_x6(h, find_conv(h, net, "conv5_3_CPM_L1"), find_conv(h, net, "conv5_3_CPM_L2"), N, hl, wl, t_(1, 0),
-                t_(0, 0), t_(1, 16), t_(0, 16), true, true);
-    run_conv_x6(h, find_conv(h, net, "conv5_4_CPM_L1"), find_conv(h, net, "conv5_4_CPM_L2"), N, hl, wl, t_(0, 0),
-                u_(0), t_(0, 16), u_(64), true, true);
-    run_conv_x6(h, find_conv(h, net, "conv5_5_CPM_L1"), find_conv(h, net, "conv5_5_CPM_L2"), N, hl, wl, u_(0),
-                s_(1, 0), u_(64), s_(1, 5), false, false);
+    const size_t ns = segs.size();
+    // per segment: S (stage inputs) and T (branch activations): padded X6P, read by the 7x7 / 3x3
+    // convs; U (conv5_4 output, read by the 1x1 conv5_5): dense
+    struct Bufs {
+        uint8_t *S[2], *T[2], *U;
+        float* O;
+        int N, hl, wl;
+    };
+    std::vector<Bufs> bs(ns);
+    std::vector<XAct> last, dup;
+    for (size_t i = 0; i < ns; ++i) {
+        auto& w = h->ws[segs[i].slot];
+        Bufs& b = bs[i];
+        b.N = segs[i].N;
+        b.hl = segs[i].Hp / 8;
+        b.wl = segs[i].Wp / 8;
+        const size_t px = (size_t)b.N * b.hl * b.wl, plane = x6p_plane(b.N, b.hl, b.wl);
+        b.S[0] = w.x6S0.ensure<uint8_t>(plane * SG * 48, h->stream);
+        b.S[1] = w.x6S1.ensure<uint8_t>(plane * SG * 48, h->stream);
+        b.T[0] = w.x6T0.ensure<uint8_t>(plane * TG * 48, h->stream);
+        b.T[1] = w.x6T1.ensure<uint8_t>(plane * TG * 48, h->stream);
+        b.U = w.x6U.ensure<uint8_t>(px * UG * 48, h->stream);
+        b.O = w.S0.ensure<float>(px * 185, h->stream);
+        clear_x6p_pads(h, {{&w.x6S0, SG}, {&w.x6S1, SG}, {&w.x6T0, TG}, {&w.x6T1, TG}}, b.N, b.hl, b.wl);
+        last.push_back(x6pact(b.S[0], SG, 8, b.N, b.hl, b.wl));
+        dup.push_back(x6pact(b.S[1], SG, 8, b.N, b.hl, b.wl));
+    }
+    auto s_ = [&](size_t i, int k, int goff) { return x6pact(bs[i].S[k], SG, goff, bs[i].N, bs[i].hl, bs[i].wl); };
+    auto t_ = [&](size_t i, int k, int goff) { return x6pact(bs[i].T[k], TG, goff, bs[i].N, bs[i].hl, bs[i].wl); };
+    auto u_ = [&](size_t i, int goff) { return x6act(bs[i].U, UG, goff, bs[i].N, bs[i].hl, bs[i].wl); };
+    // one layer over every segment: branch L1 (conv c1) and, when c2, branch L2
+    auto layer = [&](const std::string& n1, const std::string& n2, const std::function<XAct(size_t)>& in1,
+                     const std::function<XAct(size_t)>& out1, const std::function<XAct(size_t)>& in2,
+                     const std::function<XAct(size_t)>& out2, bool relu1, bool relu2) {
+        DevConv* c1 = find_conv(h, net, n1);
+        DevConv* c2 = n2.empty() ? nullptr : find_conv(h, net, n2);
+        std::vector<ConvSeg> cs;
+        for (size_t i = 0; i < ns; ++i) {
+            cs.push_back(ConvSeg{c1, bs[i].N, bs[i].hl, bs[i].wl, in1(i), out1(i), XAct{}, relu1});
+            if (c2) cs.push_back(ConvSeg{c2, bs[i].N, bs[i].hl, bs[i].wl, in2(i), out2(i), XAct{}, relu2});
+        }
+        run_conv_x6_segs(h, cs);
+    };
+    auto none = [](size_t) { return XAct{}; };
+    run_trunk_x6(h, net, segs, last, dup);
+    layer("conv5_1_CPM_L1+L2", "", [&](size_t i) { return s_(i, 0, 8); }, [&](size_t i) { return t_(i, 0, 0); }, none,
+          none, true, false);
+    layer("conv5_2_CPM_L1", "conv5_2_CPM_L2", [&](size_t i) { return t_(i, 0, 0); },
+          [&](size_t i) { return t_(i, 1, 0); }, [&](size_t i) { return t_(i, 0, 16); },
+          [&](size_t i) { return t_(i, 1, 16); }, true, true);
+    layer("conv5_3_CPM_L1", "conv5_3_CPM_L2", [&](size_t i) { return t_(i, 1, 0); },
+          [&](size_t i) { return t_(i, 0, 0); }, [&](size_t i) { return t_(i, 1, 16); },
+          [&](size_t i) { return t_(i, 0, 16); }, true, true);
+    layer("conv5_4_CPM_L1", "conv5_4_CPM_L2", [&](size_t i) { return t_(i, 0, 0); }, [&](size_t i) { return u_(i, 0); },
+          [&](size_t i) { return t_(i, 0, 16); }, [&](size_t i) { return u_(i, 64); }, true, true);
+    layer("conv5_5_CPM_L1", "conv5_5_CPM_L2", [&](size_t i) { return u_(i, 0); }, [&](size_t i) { return s_(i, 1, 0); },
+          [&](size_t i) { return u_(i, 64); }, [&](size_t i) { return s_(i, 1, 5); }, false, false);
     int cur = 1;
     for (int st = 2; st <= 6; ++st) {
         const std::string sf = "_stage" + std::to_string(st);
-        run_conv_x6(h, find_conv(h, net, "Mconv1" + sf + "_L1+L2"), nullptr, N, hl, wl, s_(cur, 0), t_(0, 0),
-                    XAct{}, XAct{}, true, false);
+        layer("Mconv1" + sf + "_L1+L2", "", [&](size_t i) { return s_(i, cur, 0); },
+              [&](size_t i) { return t_(i, 0, 0); }, none, none, true, false);
         int t = 0;
-        for (int i = 2; i <= 6; ++i) {
-            const std::string nm = "Mconv" + std::to_string(i) + sf;
-            run_conv_x6(h, find_conv(h, net, nm + "_L1"), find_conv(h, net, nm + "_L2"), N, hl, wl, t_(t, 0),
-                        t_(t ^ 1, 0), t_(t, 16), t_(t ^ 1, 16), true, true);
+        for (int k = 2; k <= 6; ++k) {
+            const std::string nm = "Mconv" + std::to_string(k) + sf;
+            layer(nm + "_L1", nm + "_L2", [&](size_t i) { return t_(i, t, 0); },
+                  [&](size_t i) { return t_(i, t ^ 1, 0); }, [&](size_t i) { return t_(i, t, 16); },
+                  [&](size_t i) { return t_(i, t ^ 1, 16); }, true, true);
             t ^= 1;
         }
-        const XAct o1 = st == 6 ? f32act(O, 185, 0) : s_(cur ^ 1, 0);
-        const XAct o2 = st == 6 ? f32act(O, 185, 38) : s_(cur ^ 1, 5);
-        run_conv_x6(h, find_conv(h, net, "Mconv7" + sf + "_L1"), find_conv(h, net, "Mconv7" + sf + "_L2"), N, hl, wl,
-                    t_(t, 0), o1, t_(t, 16), o2, false, st == 6);
+        // Mconv7: no ReLU, except Mconv7_stage6_L2 (no_relu list quirk, src/model.py:30-33)
+        layer("Mconv7" + sf + "_L1", "Mconv7" + sf + "_L2", [&](size_t i) { return t_(i, t, 0); },
+              [&](size_t i) { return st == 6 ? f32act(bs[i].O, 185, 0) : s_(i, cur ^ 1, 0); },
+              [&](size_t i) { return t_(i, t, 16); },
+              [&](size_t i) { return st == 6 ? f32act(bs[i].O, 185, 38) : s_(i, cur ^ 1, 5); }, false, st == 6);
         cur ^= 1;
     }
-    return O;
+    std::vector<float*> outs;
+    for (const Bufs& b : bs) outs.push_back(b.O);
+    return outs;
 }
 
-// handpose_model.forward on X6 activations; output fp32 in S0, channel stride 150 (heat [0,22))
-static float* hand_net_x6(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
-    const int hl = Hp / 8, wl = Wp / 8;
-    const size_t px = (size_t)N * hl * wl;
+// handpose_model.forward on X6 activations, every segment in lockstep; per segment the fp32
+// output in its slot's S0, channel stride 150 (heat [0,22))
+static std::vector<float*> hand_net_x6(opose_ctx* h, const std::vector<NetSeg>& segs) {
     const int SG = 19, TG = 16, UG = 64;  // [L 22 + 2 | trunk 128] = 3 + 16 groups; 128 / 512 channels
-    const size_t plane = x6p_plane(N, hl, wl);
-    uint8_t* S[2] = {h->w().x6S0.ensure<uint8_t>(plane * SG * 48, h->stream),
-                     h->w().x6S1.ensure<uint8_t>(plane * SG * 48, h->stream)};
-    uint8_t* T[2] = {h->w().x6T0.ensure<uint8_t>(plane * TG * 48, h->stream),
-                     h->w().x6T1.ensure<uint8_t>(plane * TG * 48, h->stream)};
-    uint8_t* U = h->w().x6U.ensure<uint8_t>(px * UG * 48, h->stream);
-    float* O = h->w().S0.ensure<float>(px * 150, h->stream);
-    clear_x6p_pads(h, {{&h->w().x6S0, SG}, {&h->w().x6S1, SG}, {&h->w().x6T0, TG}, {&h->w().x6T1, TG}}, N, hl, wl);
     const int net = OPOSE_NET_HAND;
-    auto s_ = [&](int i, int goff) { return x6pact(S[i], SG, goff, N, hl, wl); };
-    auto t_ = [&](int i) { return x6pact(T[i], TG, 0, N, hl, wl); };
-    const XAct u = x6act(U, UG, 0, N, hl, wl);
-    run_trunk_x6(h, net, x, N, Hp, Wp, s_(0, 3), s_(1, 3));
-    run_conv_x6(h, find_conv(h, net, "conv6_1_CPM"), nullptr, N, hl, wl, s_(0, 3), u, XAct{}, XAct{}, true, false);
-    run_conv_x6(h, find_conv(h, net, "conv6_2_CPM"), nullptr, N, hl, wl, u, s_(1, 0), XAct{}, XAct{}, false, false);
+    const size_t ns = segs.size();
+    struct Bufs {
+        uint8_t *S[2], *T[2], *U;
+        float* O;
+        int N, hl, wl;
+    };
+    std::vector<Bufs> bs(ns);
+    std::vector<XAct> last, dup;
+    for (size_t i = 0; i < ns; ++i) {
+        auto& w = h->ws[segs[i].slot];
+        Bufs& b = bs[i];
+        b.N = segs[i].N;
+        b.hl = segs[i].Hp / 8;
+        b.wl = segs[i].Wp / 8;
+        const size_t px = (size_t)b.N * b.hl * b.wl, plane = x6p_plane(b.N, b.hl, b.wl);
+        b.S[0] = w.x6S0.ensure<uint8_t>(plane * SG * 48, h->stream);
+        b.S[1] = w.x6S1.ensure<uint8_t>(plane * SG * 48, h->stream);
+        b.T[0] = w.x6T0.ensure<uint8_t>(plane * TG * 48, h->stream);
+        b.T[1] = w.x6T1.ensure<uint8_t>(plane * TG * 48, h->stream);
+        b.U = w.x6U.ensure<uint8_t>(px * UG * 48, h->stream);
+        b.O = w.S0.ensure<float>(px * 150, h->stream);
+        clear_x6p_pads(h, {{&w.x6S0, SG}, {&w.x6S1, SG}, {&w.x6T0, TG}, {&w.x6T1, TG}}, b.N, b.hl, b.wl);
+        last.push_back(x6pact(b.S[0], SG, 3, b.N, b.hl, b.wl));
+        dup.push_back(x6pact(b.S[1], SG, 3, b.N, b.hl, b.wl));
+    }
+    auto s_ = [&](size_t i, int k, int goff) { return x6pact(bs[i].S[k], SG, goff, bs[i].N, bs[i].hl, bs[i].wl); };
+    auto t_ = [&](size_t i, int k) { return x6pact(bs[i].T[k], TG, 0, bs[i].N, bs[i].hl, bs[i].wl); };
+    auto u_ = [&](size_t i) { return x6act(bs[i].U, UG, 0, bs[i].N, bs[i].hl, bs[i].wl); };
+    auto layer = [&](const std::string& name, const std::function<XAct(size_t)>& in,
+                     const std::function<XAct(size_t)>& out, bool relu) {
+        DevConv* c = find_conv(h, net, name);
+        std::vector<ConvSeg> cs;
+        for (size_t i = 0; i < ns; ++i) cs.push_back(ConvSeg{c, bs[i].N, bs[i].hl, bs[i].wl, in(i), out(i), XAct{}, relu});
+        run_conv_x6_segs(h, cs);
+    };
+    run_trunk_x6(h, net, segs, last, dup);
+    layer("conv6_1_CPM", [&](size_t i) { return s_(i, 0, 3); }, u_, true);
+    layer("conv6_2_CPM", u_, [&](size_t i) { return s_(i, 1, 0); }, false);
     int cur = 1;
     for (int st = 2; st <= 6; ++st) {
         const std::string sf = "_stage" + std::to_string(st);
-        run_conv_x6(h, find_conv(h, net, "Mconv1" + sf), nullptr, N, hl, wl, s_(cur, 0), t_(0), XAct{}, XAct{}, true,
-                    false);
+        layer("Mconv1" + sf, [&](size_t i) { return s_(i, cur, 0); }, [&](size_t i) { return t_(i, 0); }, true);
         int t = 0;
-        for (int i = 2; i <= 6; ++i) {
-            run_conv_x6(h, find_conv(h, net, "Mconv" + std::to_string(i) + sf), nullptr, N, hl, wl, t_(t), t_(t ^ 1),
-                        XAct{}, XAct{}, true, false);
+        for (int k = 2; k <= 6; ++k) {
+            layer("Mconv" + std::to_string(k) + sf, [&](size_t i) { return t_(i, t); },
+                  [&](size_t i) { return t_(i, t ^ 1); }, true);
             t ^= 1;
         }
-        const XAct o = st == 6 ? f32act(O, 150, 0) : s_(cur ^ 1, 0);
-        run_conv_x6(h, find_conv(h, net, "Mconv7" + sf), nullptr, N, hl, wl, t_(t), o, XAct{}, XAct{}, false, false);
+        layer("Mconv7" + sf, [&](size_t i) { return t_(i, t); },
+              [&](size_t i) { return st == 6 ? f32act(bs[i].O, 150, 0) : s_(i, cur ^ 1, 0); }, false);
         cur ^= 1;
     }
-    return O;
+    std::vector<float*> outs;
+    for (const Bufs& b : bs) outs.push_back(b.O);
+    return outs;
 }
 
 // bodypose_model.forward (src/model.py:106-133). Output: S-buffer with paf [0,38), heat [38,57)
 static float* body_net(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
     if (!h->loaded[OPOSE_NET_BODY]) throw std::runtime_error("body weights not loaded");
-    if (h->x6) return body_net_x6(h, x, N, Hp, Wp);
+    if (h->x6) return body_net_x6(h, {NetSeg{x, N, Hp, Wp, h->slot}})[0];
     const int hl = Hp / 8, wl = Wp / 8;
     const size_t px = (size_t)N * hl * wl;
     float* S[2] = {h->w().S0.ensure<float>(px * 185, h->stream), h->w().S1.ensure<float>(px * 185, h->stream)};
@@ -997,7 +1189,7 @@ static float* body_net(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
 // handpose_model.forward (src/model.py:197-214). Output: S-buffer with heat [0,22)
 static float* hand_net(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
     if (!h->loaded[OPOSE_NET_HAND]) throw std::runtime_error("hand weights not loaded");
-    if (h->x6) return hand_net_x6(h, x, N, Hp, Wp);
+    if (h->x6) return hand_net_x6(h, {NetSeg{x, N, Hp, Wp, h->slot}})[0];
     const int hl = Hp / 8, wl = Wp / 8;
     const size_t px = (size_t)N * hl * wl;
     float* S[2] = {h->w().S0.ensure<float>(px * 150, h->stream), h->w().S1.ensure<float>(px * 150, h->stream)};
@@ -1131,6 +1323,28 @@ static void upsample_to_mid(opose_ctx* h, int s, const float* maps, int cstride,
     h->prof_begin(pe, "upsample8", 0, (double)N * C * g.Hs * g.Ws * 4);
     launch_upsample8(maps, cstride, 0, C, N, g.hl, g.wl, g.Hs, g.Ws, mid, h->stream);
     h->prof_end(pe);
+}
+
+// Every scale's network in lockstep on the handle's stream (split-bf16 path): per scale the
+// preprocess into its slot's input, one conv launch per layer for all scales (hand_net_x6 /
+// body_net_x6 segments), per scale the x8 upsample of its C heat / PAF channels into mid(s).
+static void run_scales_lockstep(opose_ctx* h, int net, const uint8_t* fd, int64_t frame_stride, int64_t row_stride,
+                                int N, int H, int W, const std::vector<ScaleGeom>& gs, const opose_params& p) {
+    if (!h->loaded[net]) throw std::runtime_error(net == OPOSE_NET_BODY ? "body weights not loaded" : "hand weights not loaded");
+    std::vector<NetSeg> segs;
+    for (size_t s = 0; s < gs.size(); ++s) {
+        const ScaleGeom& g = gs[s];
+        float* x = h->ws[s].x.ensure<float>((size_t)N * 3 * g.Hp * g.Wp, h->stream);
+        ProfEntry pe;
+        h->prof_begin(pe, "preprocess", 0, (double)N * (3.0 * H * W + 12.0 * g.Hp * g.Wp));
+        launch_preprocess(fd, frame_stride, row_stride, N, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp, g.Wp,
+                          (float)p.pad_value / 256.f - 0.5f, x, h->stream);
+        h->prof_end(pe);
+        segs.push_back(NetSeg{x, N, g.Hp, g.Wp, (int)s});
+    }
+    const std::vector<float*> outs = net == OPOSE_NET_BODY ? body_net_x6(h, segs) : hand_net_x6(h, segs);
+    for (size_t s = 0; s < gs.size(); ++s)
+        upsample_to_mid(h, (int)s, outs[s], net == OPOSE_NET_BODY ? 185 : 150, N, gs[s], net == OPOSE_NET_BODY ? 56 : 21);
 }
 
 // bytes a strided uint8 [N][H][W][3] host view spans: the last row ends 3*W bytes after its start,
@@ -1496,6 +1710,47 @@ static int net_forward(opose_t* h, int net, const float* x, int N, int Hp, int W
     return OPOSE_OK;
 }
 
+int opose_hand_forward_pyramid(opose_t* h, int n, const float* const* xs, const int* N, const int* Hp, const int* Wp,
+                               float* const* heats, int flags) {
+    if (!h || !xs || !N || !Hp || !Wp || !heats || n < 1 || n > OPOSE_MAX_SCALES) return OPOSE_E_ARG;
+    for (int i = 0; i < n; ++i)
+        if (!xs[i] || !heats[i] || N[i] <= 0 || Hp[i] < 8 || Wp[i] < 8 || Hp[i] % 8 || Wp[i] % 8) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        enter_main(h);
+        if (!h->loaded[OPOSE_NET_HAND]) throw std::runtime_error("hand weights not loaded");
+        const hipMemcpyKind kind = (flags & OPOSE_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        std::vector<NetSeg> segs;
+        for (int i = 0; i < n; ++i) {
+            const size_t in_n = (size_t)N[i] * 3 * Hp[i] * Wp[i];
+            const float* xd = xs[i];
+            if (!(flags & OPOSE_IN_DEVICE)) {
+                float* buf = h->ws[i].x.ensure<float>(in_n, h->stream);
+                OPOSE_HIP_CHECK(hipMemcpyAsync(buf, xs[i], in_n * 4, hipMemcpyHostToDevice, h->stream));
+                xd = buf;
+            }
+            segs.push_back(NetSeg{xd, N[i], Hp[i], Wp[i], i});
+        }
+        std::vector<float*> outs;
+        if (h->x6) {
+            outs = hand_net_x6(h, segs);
+        } else {
+            for (int i = 0; i < n; ++i) {
+                h->slot = i;
+                outs.push_back(hand_net(h, segs[i].x, N[i], Hp[i], Wp[i]));
+            }
+            h->slot = 0;
+        }
+        for (int i = 0; i < n; ++i) {
+            const size_t plane = (size_t)(Hp[i] / 8) * (Wp[i] / 8);
+            OPOSE_HIP_CHECK(hipMemcpy2DAsync(heats[i], 22 * plane * 4, outs[i], 150 * plane * 4, 22 * plane * 4, N[i],
+                                             kind, h->stream));
+        }
+        if (!(flags & OPOSE_OUT_DEVICE)) OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+        h->prof_drain();
+    });
+    return OPOSE_OK;
+}
+
 int opose_body_forward(opose_t* h, const float* x, int N, int Hp, int Wp, float* paf, float* heat, int flags) {
     if (!paf || !heat) return OPOSE_E_ARG;
     return net_forward(h, OPOSE_NET_BODY, x, N, Hp, Wp, paf, heat, flags);
@@ -1631,15 +1886,18 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
             float* S = body_net(h, x, N, g.Hp, g.Wp);
             upsample_to_mid(h, s, S, 185, N, g, 56);
         };
+        const bool lockstep = h->x6 && h->lockstep == 2 && p.n_scales > 1;
         auto net_part = [&] {
-            if (h->scale_streams && p.n_scales > 1)  // (pipelined: forked from and joined into nstream)
+            if (lockstep)
+                run_scales_lockstep(h, OPOSE_NET_BODY, fd, frame_stride, row_stride, N, H, W, gs, p);
+            else if (h->scale_streams && p.n_scales > 1)  // (pipelined: forked from and joined into nstream)
                 run_scales_concurrently(h, p.n_scales, scale_net);
             else
                 for (int s = 0; s < p.n_scales; ++s) scale_net(s);
         };
         if ((flags & OPOSE_PIPELINE) && (flags & OPOSE_IN_DEVICE) && (flags & OPOSE_OUT_DEVICE)) {
             pipelined_body(h, N, H, W, gs, p, rec, net_part);
-        } else if (h->scale_streams && p.n_scales > 1) {  // multi-scale pyramid (C5): scales concurrently
+        } else if (!lockstep && h->scale_streams && p.n_scales > 1) {  // multi-scale pyramid (C5): scales concurrently
             enter_main(h);
             h->mid_set = 0;
             run_scales_concurrently(h, p.n_scales, scale_net);
@@ -1921,7 +2179,12 @@ int opose_hand_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
             float* Sb = hand_net(h, x, N, g.Hp, g.Wp);
             upsample_to_mid(h, s, Sb, 150, N, g, 21);
         };
-        if (h->scale_streams && p.n_scales > 1) {
+        if (h->x6 && h->lockstep && p.n_scales > 1) {
+            run_graphed(h, key, [&] {
+                run_scales_lockstep(h, OPOSE_NET_HAND, fd, frame_stride, row_stride, N, H, W, gs, p);
+                hand_post_common(h, N, H, W, gs, p, peaks, found, flags & OPOSE_OUT_DEVICE);
+            });
+        } else if (h->scale_streams && p.n_scales > 1) {
             // the scales' networks are independent until the heat average: each on its own stream
             // with its own workspace (a single crop's layers fill a fraction of the chip each)
             run_scales_concurrently(h, p.n_scales, scale_net);
@@ -2038,9 +2301,14 @@ int opose_hand_infer_crops(opose_t* h, const uint8_t* const* crops, const int* s
                 OPOSE_HIP_CHECK(hipMemcpyAsync(buf + off[i], crops[i], host_span(1, sizes[i], sizes[i], row_strides[i], 0),
                                                hipMemcpyHostToDevice, h->stream));
         }
+        // all crops of a scale form one batch; with the split-bf16 path all scales run in lockstep
+        // (one conv launch per layer for every crop and scale)
+        const bool lockstep = h->x6 && h->lockstep && ns > 1;
+        if (lockstep && !h->loaded[OPOSE_NET_HAND]) throw std::runtime_error("hand weights not loaded");
+        std::vector<NetSeg> segs;
         for (int s = 0; s < ns; ++s) {
             const ScaleGeom& g0 = gs[0][s];
-            float* x = h->w().x.ensure<float>((size_t)n * 3 * g0.Hp * g0.Wp, h->stream);
+            float* x = h->ws[lockstep ? s : h->slot].x.ensure<float>((size_t)n * 3 * g0.Hp * g0.Wp, h->stream);
             ProfEntry pe;
             h->prof_begin(pe, "preprocess", 0, 0);
             for (int i = 0; i < n; ++i) {
@@ -2051,8 +2319,16 @@ int opose_hand_infer_crops(opose_t* h, const uint8_t* const* crops, const int* s
                                   x + (size_t)i * 3 * g.Hp * g.Wp, h->stream);
             }
             h->prof_end(pe);
+            if (lockstep) {
+                segs.push_back(NetSeg{x, n, g0.Hp, g0.Wp, s});
+                continue;
+            }
             float* Sb = hand_net(h, x, n, g0.Hp, g0.Wp);
             upsample_to_mid(h, s, Sb, 150, n, g0, 21);
+        }
+        if (lockstep) {
+            const std::vector<float*> outs = hand_net_x6(h, segs);
+            for (int s = 0; s < ns; ++s) upsample_to_mid(h, s, outs[s], 150, n, gs[0][s], 21);
         }
         (void)base;
         // size every per-crop buffer for the largest crop / all crops up front: a reallocation
@@ -2132,7 +2408,7 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
         G.in = xd; G.in_cstride = Cin; G.in_coff = 0; G.wt = c->wt; G.bias = c->bias;
         G.out = yd; G.out_cstride = Cout; G.out_coff = 0; G.out2 = nullptr; G.cout = Cout; G.relu = relu;
         a.g[1] = a.g[0];
-        TileChoice t = choose_tile(a.Mpad, a.npix, 1, a.Kpad / 32);
+        TileChoice t = choose_tile(a.Mpad, {a.npix}, a.Kpad / 32);
         if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((a.npix + pt - 1) / pt); }
         if (splits > 0) t.grid = splits;
         if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
@@ -2169,16 +2445,16 @@ int opose_debug_conv_x6(opose_t* h, const float* x, const float* w, const float*
         OPOSE_HIP_CHECK(hipMemcpyAsync(xd, x, nx * 4, hipMemcpyHostToDevice, h->stream));
         launch_to_x6(xd, Cin, 0, Cin, N, HW, x6, cg, 0, ips, h->stream);
         X6Args a{};
-        a.N = N; a.H = H; a.W = W; a.ks = ks; a.pad = pad;
-        a.cin_g = cg; a.small = c->small6 ? 1 : 0; a.nK = c->nK6; a.Mpad = c->Mpad; a.npix = N * HW;
+        a.ks = ks; a.pad = pad;
+        a.cin_g = cg; a.small = c->small6 ? 1 : 0; a.nK = c->nK6; a.Mpad = c->Mpad;
         X6Group& G = a.g[0];
+        G.N = N; G.H = H; G.W = W; G.npix = N * HW;
         G.in = x6; G.in_ps = ips; G.in_l = x6act(x6, cg, 0, N, H, W).l;
         G.wt = c->wx6; G.bias = c->bias; G.cout = Cout; G.relu = relu; G.out2 = nullptr;
         if (out_x6) { G.out = y6; G.out_ps = ops; G.out_l = x6act(y6, og, 0, N, H, W).l; G.out_f32 = 0; }
         else { G.out = yd; G.out_c = Cout; G.out_off = 0; G.out_f32 = 1; }
-        a.g[1] = a.g[0];
-        TileChoice t = choose_tile(a.Mpad, a.npix, 1, a.nK, true);
-        if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((a.npix + pt - 1) / pt); }
+        TileChoice t = choose_tile(a.Mpad, {G.npix}, a.nK, true);
+        if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((G.npix + pt - 1) / pt); }
         if (splits > 0) t.grid = splits;
         if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
         a.ngroups = 1;
@@ -2215,18 +2491,19 @@ int opose_debug_conv_x6_time(opose_t* h, int N, int Cin, int H, int W, int Cout,
         uint8_t* y6 = yx.ensure<uint8_t>((size_t)ops * 3, h->stream);
         launch_to_x6(xd, cg * 8, 0, cg * 8, ngroups * N, HW, x6, cg, 0, ips, h->stream);
         X6Args a{};
-        a.N = N; a.H = H; a.W = W; a.ks = ks; a.pad = ks / 2;
-        a.cin_g = cg; a.small = c->small6 ? 1 : 0; a.nK = c->nK6; a.Mpad = c->Mpad; a.npix = N * HW;
-        for (int g = 0; g < 2; ++g) {
+        a.ks = ks; a.pad = ks / 2;
+        a.cin_g = cg; a.small = c->small6 ? 1 : 0; a.nK = c->nK6; a.Mpad = c->Mpad;
+        for (int g = 0; g < ngroups; ++g) {
             X6Group& G = a.g[g];
-            const int gg = g < ngroups ? g : 0;
+            const int gg = g;
+            G.N = N; G.H = H; G.W = W; G.npix = N * HW;
             G.in = x6 + (size_t)gg * N * cg * HW * 16; G.in_ps = ips; G.in_l = x6act(x6, cg, 0, N, H, W).l;
             G.wt = c->wx6; G.bias = c->bias; G.cout = Cout; G.relu = 1; G.out2 = nullptr;
             G.out = y6 + (size_t)gg * N * og * HW * 16; G.out_ps = ops; G.out_l = x6act(y6, og, 0, N, H, W).l;
             G.out_f32 = 0;
         }
-        TileChoice t = choose_tile(a.Mpad, a.npix, ngroups, a.nK, true);
-        if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((a.npix + pt - 1) / pt) * ngroups; }
+        TileChoice t = choose_tile(a.Mpad, std::vector<int>(ngroups, N * HW), a.nK, true);
+        if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((N * HW + pt - 1) / pt) * ngroups; }
         if (splits > 0) t.grid = splits;
         if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
         a.ngroups = ngroups;
@@ -2276,7 +2553,7 @@ int opose_debug_conv_time(opose_t* h, int N, int Cin, int H, int W, int Cout, in
             G.out = yd + (size_t)gg * N * Cout * H * W; G.out_cstride = Cout; G.out_coff = 0; G.out2 = nullptr;
             G.cout = Cout; G.relu = 1;
         }
-        TileChoice t = choose_tile(a.Mpad, a.npix, ngroups, a.Kpad / 32);
+        TileChoice t = choose_tile(a.Mpad, std::vector<int>(ngroups, a.npix), a.Kpad / 32);
         if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((a.npix + pt - 1) / pt) * ngroups; }
         if (splits > 0) t.grid = splits;
         if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");

@@ -30,6 +30,10 @@ void launch_maxpool(const float* in, float* out, int NC, int H, int W, hipStream
 // conv_x6.hip (split-bf16 fp32-accurate convolution, X6 activation format: common.h)
 void x6_pack_weights(const float* w, int cout, int cin, int ks, int Mpad, int* nK_out, std::vector<uint16_t>& out);
 void launch_conv_x6(const X6Args& a, int mt, int pt, hipStream_t st);
+// X6Args with the groups' tiles numbered for an mt x pt tile (X6Group::t0, X6Args::tiles)
+X6Args x6_number_tiles(const X6Args& a, int mt, int pt);
+// stream-K fixup of a 128 x 256 tile grid (conv_win_x6)
+void launch_conv_x6_fixup(const X6Args& a, int mt, int pt, hipStream_t st);
 void launch_to_x6(const float* in, int cstride, int coff, int C, int N, int HW, uint8_t* out, int cg, int goff,
                   uint32_t ps, hipStream_t st);
 void launch_from_x6(const uint8_t* in, int cg, int goff, uint32_t ps, int C, int N, int HW, float* out, int cstride,
@@ -43,8 +47,9 @@ void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t o
 // conv1_2 (64 -> 64, 3x3 pad 1) + MaxPool2d(2, 2) from an 8-group X6 tensor, input window in LDS
 void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int W, const uint8_t* wt,
                               const float* bias, uint8_t* out, uint32_t ops, hipStream_t st);
-// conv_win.hip: the 7x7 CPM convs with the im2col operand from an LDS window of the padded X6P
-// input (pair-order weights: x6_pack_weights_pairs); whole 128 x 256 tiles
+// conv_win.hip: the 7x7 / 3x3 convs with the im2col operand from an LDS window of the padded X6P
+// input (pair-order weights: x6_pack_weights_pairs); 128 x 256 tiles, data parallel
+// (sk_grid == tiles) or stream-K
 void x6_pack_weights_pairs(const float* w, int cout, int cin, int ks, int Mpad, int* nK_out,
                            std::vector<uint16_t>& out);
 bool conv_win_fits(int N, int H, int W, int ks);

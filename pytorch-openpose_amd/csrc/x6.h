@@ -53,6 +53,13 @@ __device__ __forceinline__ uint32_t x6_unit(const X6Layout& l, int n, int g, int
     return l.o0 + (uint32_t)n * l.fs + (uint32_t)g * l.gs + (uint32_t)y * l.rs + (uint32_t)x;
 }
 
+// group of a tile (groups are numbered in tile order, X6Group::t0)
+__device__ __forceinline__ int x6_group_of(const X6Args& a, int tile) {
+    int g = 0;
+    for (int i = 1; i < a.ngroups; ++i) g = tile >= a.g[i].t0 ? i : g;
+    return g;
+}
+
 }  // namespace x6
 using namespace x6;
 

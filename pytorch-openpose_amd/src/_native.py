@@ -47,6 +47,7 @@ def _load():
         "opose_load_weights": (I, [P, I, C.POINTER(P), P, I]),
         "opose_body_forward": (I, [P, P, I, I, I, P, P, I]),
         "opose_hand_forward": (I, [P, P, I, I, I, P, I]),
+        "opose_hand_forward_pyramid": (I, [P, I, C.POINTER(P), P, P, P, C.POINTER(P), I]),
         "opose_body_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, I]),
         "opose_body_post": (I, [P, P, I, I, I, I, I, I, I, C.POINTER(Params), P, I]),
         "opose_body_scale_geom": (I, [I, I, C.POINTER(Params), I, P]),
@@ -70,6 +71,8 @@ def _load():
         "opose_debug_heat": (I, [P, P, I, I, I, I, I, I, P, P]),
     }
     for name, (res, args) in sig.items():
+        if "OPOSE_LIB" in os.environ and not hasattr(lib, name):
+            continue  # an older build picked for a same-box A/B may predate later entry points
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -82,7 +85,8 @@ lib = _load()
 EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last_error", "opose_set_stream",
             "opose_wait_stream", "opose_signal_stream",
             "opose_get_stream", "opose_synchronize", "opose_set_capacity", "opose_body_record_bytes",
-            "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_body_infer",
+            "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_hand_forward_pyramid",
+            "opose_body_infer",
             "opose_body_post", "opose_body_scale_geom", "opose_body_scale_maps",
             "opose_body_post_scales", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
             "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_conv_time", "opose_debug_conv_x6", "opose_debug_conv_x6_time", "opose_debug_preprocess",

@@ -156,3 +156,21 @@ class handpose_model(_DeviceNet):
         heat = np.empty((N, 22, H // 8, W // 8), np.float32)
         self.handle.check(_native.lib.opose_hand_forward(self.handle.h, xn.ctypes.data, N, H, W, heat.ctypes.data, 0))
         return heat
+
+    def forward_pyramid(self, xs):
+        """The networks of a scale pyramid in one lockstep pass (what Hand() runs for its
+        scale_search): xs = list of [N,3,H,W] fp32 host arrays -> list of heat [N,22,H/8,W/8]
+        (opose_hand_forward_pyramid; one conv launch per layer covers every scale)."""
+        import ctypes as C
+        xn = [np.ascontiguousarray(x, dtype=np.float32) for x in xs]
+        for x in xn:
+            if x.ndim != 4 or x.shape[1] != 3 or x.shape[2] % 8 or x.shape[3] % 8:
+                raise ValueError("inputs must be [N,3,H,W] with H, W multiples of 8")
+        heats = [np.empty((x.shape[0], 22, x.shape[2] // 8, x.shape[3] // 8), np.float32) for x in xn]
+        n = len(xn)
+        P = C.c_void_p * n
+        Iv = C.c_int * n
+        self.handle.check(_native.lib.opose_hand_forward_pyramid(
+            self.handle.h, n, P(*[x.ctypes.data for x in xn]), Iv(*[x.shape[0] for x in xn]),
+            Iv(*[x.shape[2] for x in xn]), Iv(*[x.shape[3] for x in xn]), P(*[o.ctypes.data for o in heats]), 0))
+        return heats

@@ -210,3 +210,55 @@ def test_conv7_window_vs_im2col(native, kind, shape):
         tol = 2e-4 * np.abs(r).max() + 2e-4 * np.abs(r)
         assert (np.abs(a - r) <= tol).all()
         assert np.abs(a - r).max() <= 5e-5 * np.abs(r).max()
+
+
+def _hand_model(env):
+    from src import util
+    from src.model import handpose_model
+    from src.weights import seeded_state_dict
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        m = handpose_model(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    m.load_state_dict(util.transfer(m, seeded_state_dict("hand", 0)))
+    return m
+
+
+@pytest.mark.parametrize("crops,sizes", [(1, (184, 368, 552, 736)), (2, (184, 368, 552, 736)), (3, (48, 96, 144))],
+                         ids=["one_crop_368", "two_crops_368", "three_crops_96"])
+@pytest.mark.parametrize("env", [{}, {"OPOSE_WIN_SK": "0"}, {"OPOSE_CONV7_WIN": "0"}],
+                         ids=["default", "window_dp_only", "no_window"])
+def test_hand_pyramid_lockstep_vs_per_scale(native, crops, sizes, env):
+    """Hand()'s scale pyramid in lockstep (opose_hand_forward_pyramid: one conv launch per layer
+    for every scale, X6 groups of different geometry in one grid -- stream-K conv_x6 or conv_win_x6
+    ranges crossing from one scale's tiles into the next) against each scale's network on its own
+    (opose_hand_forward): fp32 summation-order noise only (the planner splits k at other points).
+    The 368-crop pyramid is C3's; three 96-crops the crop-batched Hand of a frame with hands."""
+    rng = np.random.default_rng(17)
+    xs = [rng.random((crops, 3, s, s), dtype=np.float32) - np.float32(0.5) for s in sizes]
+    m = _hand_model(env)
+    pyr = m.forward_pyramid(xs)
+    for x, a in zip(xs, pyr):
+        r = m(x)
+        tol = 2e-4 * np.abs(r).max() + 2e-4 * np.abs(r)
+        assert (np.abs(a - r) <= tol).all()
+        assert np.abs(a - r).max() <= 5e-5 * np.abs(r).max()
+
+
+def test_hand_pyramid_vs_oracle(native):
+    """The lockstep pyramid against the oracle network (oracle/network.py hand_forward, the
+    reference's handpose_model restated) at small sizes: the network tolerance."""
+    from oracle import network
+    sd = network.seeded_state_dict("hand", 0)
+    rng = np.random.default_rng(18)
+    xs = [rng.random((2, 3, s, s), dtype=np.float32) - np.float32(0.5) for s in (40, 80, 120, 160)]
+    pyr = _hand_model({}).forward_pyramid(xs)
+    for x, a in zip(xs, pyr):
+        r = network.hand_forward(torch.from_numpy(x), sd).numpy()
+        np.testing.assert_allclose(a, r, rtol=2e-4, atol=2e-4 * float(np.abs(r).max()))
