@@ -36,7 +36,7 @@
 
 namespace opose {
 
-template <int MT, int PT, int KS, int WMAX>
+template <int MT, int PT, int KS, int WMAX, int NST>
 __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a) {
     constexpr int TAPS = KS * KS, PAD = KS / 2;
     constexpr int NW = x6_waves(MT, PT), NWM = NW == 8 ? MT / 64 : 2, NWP = NW / NWM;
@@ -48,8 +48,12 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     // TAPS >= 9: a group ends at most once per chunk, and the window of group g + 2 (issued after
     // the last chunk of group g) lands at least one barrier before its first read
     static_assert(A_U % (64 * NW) == 0 && A_PW == 3 && WMAX % 64 == 0 && TAPS >= 9, "conv_win_x6 tile");
+    // NST weight stages: the DMA of chunk c + NST goes into chunk c's stage right after chunk c's
+    // barrier, so a stage has NST - 1 chunks to land
+    static_assert(NST == 2 || NST == 3, "conv_win_x6 stages");
+    constexpr int WOFF = NST * A_U;              // window buffers after the weight stages
 
-    __shared__ __attribute__((aligned(16))) uint4 lds[2 * A_U + 2 * WBUF];
+    __shared__ __attribute__((aligned(16))) uint4 lds[NST * A_U + 2 * WBUF];
     __shared__ float s_bias[MT];
 
     const int tid = threadIdx.x;
@@ -76,7 +80,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     const int c_begin = (int)max<long long>(0, lo - (long long)tile * nK);
     itp = (long long)tile * nK + c_begin;
     const int first = itp == lo;
-    const X6Group& G = a.g[x6_group_of(a, tile)];
+    const X6Group G = a.g[x6_group_of(a, tile)];
     const int H = G.H, W = G.W, HW = H * W, npix = G.npix;
     const int mt = (tile - G.t0) % nM;
     const int ptl = (tile - G.t0) / nM;
@@ -101,7 +105,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     // window of input group g -> buffer g & 1 (units [ws, ws + 64 NQ) of each piece plane)
     auto dma_win = [&](int g) __attribute__((always_inline)) {
         const uint32_t src = (plane0 + (uint32_t)g * G.in_l.gs + (uint32_t)ws) * 16u;
-        uint4* dst = lds + 2 * A_U + (g & 1) * WBUF;
+        uint4* dst = lds + WOFF + (g & 1) * WBUF;
         for (int i = wave; i < 3 * NQ; i += NW) {
             const int pc = i / NQ, j = i - pc * NQ;
             const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
         const int p = min(p0 + wp0 + 16 * j + (lane & 15), npix - 1);  // past the end: any window unit
         const int n = p / HW, r = p - n * HW, y = r / W, x = r - y * W;
         const int wpos = (3 + n * (H + 3) + y) * P + 3 + x - ws;
-        bbase[j] = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + 2 * A_U + wpos);
+        bbase[j] = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + WOFF + wpos);
     }
     // pair of this lane's k-group in a chunk: q = 4c + gi -> (group g, tap t), advanced by 4 per chunk
     int pg_g = (4 * c_begin + gi) / TAPS, pg_t = (4 * c_begin + gi) % TAPS;  // chunk c_begin
@@ -198,10 +202,10 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     const int g_first = (4 * c_begin) / TAPS;
     dma_win(g_first);
     if (g_first + 1 < cin_g) dma_win(g_first + 1);
-    dma_a(c_begin, 0);
-    dma_a(min(c_begin + 1, c_end - 1), 1);
+#pragma unroll
+    for (int st = 0; st < NST; ++st) dma_a(min(c_begin + st, c_end - 1), st);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // both windows and both stages landed everywhere
+    __syncthreads();  // both windows and every stage landed everywhere
     uint32_t bcur[TN], bnxt[TN];
     {
         const uint32_t off = pair_off();
@@ -216,10 +220,11 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     // group whose last chunk comes next, and that chunk: its buffer is refilled after that barrier
     int end_g = g_first;
     int end_c = (g_first * TAPS + TAPS - 1) / 4;
+    int buf = 0;  // stage of chunk c
     for (int c = c_begin; c < c_end; ++c) {
-        const int buf = (c - c_begin) & 1;
-        const uint32_t a_cur = la(buf), a_nxt = la(buf ^ 1);
-        const int c2 = min(c + 2, c_end - 1);  // past the end: a harmless reload of the last chunk
+        const int nbuf = buf + 1 == NST ? 0 : buf + 1;
+        const uint32_t a_cur = la(buf), a_nxt = la(nbuf);
+        const int c2 = min(c + NST, c_end - 1);  // past the end: a harmless reload of the last chunk
 #pragma unroll
         for (int j = 0; j < TN; ++j) bcur[j] = bnxt[j];
         advance();  // (pg_g, pg_t) -> chunk c + 1
@@ -258,10 +263,14 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
             __builtin_amdgcn_sched_barrier(0);
         }
         // this weight stage and every fragment of chunk c read by all; the next stage (and any
-        // window DMA'd since the previous barrier) landed.  The vmcnt(0) is explicit: the
-        // compiler does not count LDS-DMA as LDS writes at a workgroup barrier (it emitted a
-        // bare s_barrier here), and the fragment reads are inline asm it cannot see
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // window DMA'd since the previous barrier) landed -- with 3 stages the A_PW DMA
+        // instructions of the chunk after it (issued last) may still be in flight.  The vmcnt is
+        // explicit: the compiler does not count LDS-DMA as LDS writes at a workgroup barrier (it
+        // emitted a bare s_barrier here), and the fragment reads are inline asm it cannot see
+        if constexpr (NST == 3)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(A_PW) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         __builtin_amdgcn_sched_barrier(0);
         if (c == end_c) {  // group end_g is read for the last time: its buffer takes group end_g + 2
@@ -301,6 +310,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+        buf = nbuf;
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the last (unused) reads / loads landed
     fence_all();
@@ -403,6 +413,10 @@ void x6_pack_weights_pairs(const float* w, int cout, int cin, int ks, int Mpad, 
 
 // window capacities (units per (piece, group)): LDS = 2 weight stages (48 KB) + 2 x 3 x WMAX units
 constexpr int kWinSmall = 768, kWinLarge = 1088;
+#ifndef OPOSE_WIN_STAGES
+#define OPOSE_WIN_STAGES 3
+#endif
+constexpr int kWinStagesSmall = OPOSE_WIN_STAGES;  // weight stages of the small-window kernels
 
 // largest window (units) a tile of PT pixels needs on an N x H x W batch for a KS x KS conv
 int conv_win_units(int N, int H, int W, int ks, int pt) {
@@ -433,12 +447,12 @@ void launch_conv_win_x6(const X6Args& a0, hipStream_t st) {
     }
     if (a.sk_grid < 1 || a.sk_grid > a.tiles * a.nK) throw std::invalid_argument("conv_win_x6: bad grid");
     const dim3 grid(a.sk_grid), blk(512);
-    if (need <= kWinSmall) {
-        if (a.ks == 7) hipLaunchKernelGGL((conv_win_x6<128, 256, 7, kWinSmall>), grid, blk, 0, st, a);
-        else hipLaunchKernelGGL((conv_win_x6<128, 256, 3, kWinSmall>), grid, blk, 0, st, a);
+    if (need <= kWinSmall) {  // room for a third weight stage (48 + 72 + 24 KB of LDS)
+        if (a.ks == 7) hipLaunchKernelGGL((conv_win_x6<128, 256, 7, kWinSmall, kWinStagesSmall>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL((conv_win_x6<128, 256, 3, kWinSmall, kWinStagesSmall>), grid, blk, 0, st, a);
     } else if (need <= kWinLarge) {
-        if (a.ks == 7) hipLaunchKernelGGL((conv_win_x6<128, 256, 7, kWinLarge>), grid, blk, 0, st, a);
-        else hipLaunchKernelGGL((conv_win_x6<128, 256, 3, kWinLarge>), grid, blk, 0, st, a);
+        if (a.ks == 7) hipLaunchKernelGGL((conv_win_x6<128, 256, 7, kWinLarge, 2>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL((conv_win_x6<128, 256, 3, kWinLarge, 2>), grid, blk, 0, st, a);
     } else {
         throw std::invalid_argument("conv_win_x6: window exceeds LDS");
     }

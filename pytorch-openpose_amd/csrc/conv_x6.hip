@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         const int c_begin = (int)max<long long>(0, lo - (long long)tile * nK);
         itp = (long long)tile * nK + c_begin;
         const int first = itp == lo;
-        const X6Group& G = a.g[x6_group_of(a, tile)];
+        const X6Group G = a.g[x6_group_of(a, tile)];
         H = G.H;
         W = G.W;
         HW = H * W;
