@@ -100,6 +100,27 @@ struct X6Args {
     int pool;       // 1: 2x2/2 max-pool fused into the epilogue (npix = N * (H/2) * (W/2) * 4, quad-major)
 };
 
+// Two chained 1x1 convs (conv1x1_chain.hip): Y = W2 relu(W1 X + b1) + b2 per group (a CPM
+// branch of a scale); X: cin_g * 8 channels, W1: m1 rows, Y: cout2 <= 64 channels
+struct X6ChainGroup {
+    const uint8_t* in;           // X6 input (plane 0)
+    const uint8_t* w1;           // [cin_g/4][3][4][m1] units (x6_pack_weights)
+    const float* b1;             // [m1]
+    const uint8_t* w2;           // [m1/32][3][4][64] units
+    const float* b2;             // [cout2]
+    void* out;                   // X6 slice, or fp32 NCHW when out_f32
+    uint32_t in_ps, out_ps;
+    X6Layout in_l, out_l;
+    int out_c, out_off, out_f32;
+    int cout2, relu2;
+    int N, H, W, npix, t0;       // geometry; first tile (set by the launcher)
+};
+
+struct X6ChainArgs {
+    X6ChainGroup g[kX6Groups];
+    int cin_g, m1, ngroups, tiles;
+};
+
 // ---------------------------------------------------------------- body records
 struct RecordLayout {
     int peaks_per_part;  // capacity per part

@@ -209,6 +209,12 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_CONV7_WIN");
         return !(e && e[0] == '0');
     }();
+    // a CPM stage's closing 1x1 pair in one launch (conv1x1_chain_x6); OPOSE_FUSE_1X1=0: two
+    // launches through an HBM intermediate (the cross-check of tests/test_gpu_x6.py)
+    bool fuse1x1 = [] {
+        const char* e = getenv("OPOSE_FUSE_1X1");
+        return !(e && e[0] == '0');
+    }();
     // OPOSE_WIN_SK=0: conv_win_x6 only on data-parallel grids that fill the chip (no stream-K
     // window launches; the A/B of the planner's window pricing)
     bool win_dp_only = [] {
@@ -791,12 +797,75 @@ static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, boo
     h->prof_end(pe);
 }
 
-// the single-geometry form: one conv (c1 null) or a CPM branch pair on N x H x W
-static void run_conv_x6(opose_ctx* h, DevConv* c0, DevConv* c1, int N, int H, int W, XAct in0, XAct out0, XAct in1,
-                        XAct out1, bool relu0, bool relu1, XAct dup = XAct{}, bool pool = false) {
-    std::vector<ConvSeg> segs{ConvSeg{c0, N, H, W, in0, out0, dup, relu0}};
-    if (c1) segs.push_back(ConvSeg{c1, N, H, W, in1, out1, XAct{}, relu1});
-    run_conv_x6_segs(h, segs, pool);
+// A CPM stage's closing 1x1 pair (conv5_4 -> conv5_5, conv6_1 -> conv6_2, Mconv6 -> Mconv7) on one
+// segment: out = c2(relu(c1(in))) (+ ReLU when relu2); `mid` holds c1's output when the pair runs
+// as two launches.
+struct ChainSeg {
+    DevConv *c1, *c2;
+    int N, H, W;
+    XAct in, mid, out;
+    bool relu2;
+};
+
+// One launch of conv1x1_chain_x6 for every segment (the intermediate never leaves the CU), or,
+// with OPOSE_FUSE_1X1=0 or a shape the kernel does not take, the two convs as separate launches
+// through `mid`.
+static void run_chain_x6(opose_ctx* h, const std::vector<ChainSeg>& segs) {
+    bool fuse = h->fuse1x1 && !segs.empty() && segs.size() <= (size_t)kX6Groups;
+    for (const ChainSeg& sg : segs) {
+        const DevConv *c1 = sg.c1, *c2 = sg.c2;
+        fuse = fuse && c1->ks == 1 && c2->ks == 1 && c1->cin_g == 16 && c1->cout == c1->Mpad && c1->Mpad % 128 == 0 &&
+               c2->cin == c1->cout && c2->Mpad == 64 && c2->nK6 == c1->cout / 32 && !c1->small6 &&
+               c1->cin_g == segs[0].c1->cin_g && c1->cout == segs[0].c1->cout;
+    }
+    if (!fuse) {
+        std::vector<ConvSeg> first, second;
+        for (const ChainSeg& sg : segs) {
+            first.push_back(ConvSeg{sg.c1, sg.N, sg.H, sg.W, sg.in, sg.mid, XAct{}, true});
+            second.push_back(ConvSeg{sg.c2, sg.N, sg.H, sg.W, sg.mid, sg.out, XAct{}, sg.relu2});
+        }
+        run_conv_x6_segs(h, first);
+        run_conv_x6_segs(h, second);
+        return;
+    }
+    X6ChainArgs a{};
+    a.cin_g = segs[0].c1->cin_g;
+    a.m1 = segs[0].c1->cout;
+    a.ngroups = (int)segs.size();
+    double flops = 0;
+    long npix_all = 0;
+    for (size_t g = 0; g < segs.size(); ++g) {
+        const ChainSeg& sg = segs[g];
+        X6ChainGroup& G = a.g[g];
+        G.in = static_cast<const uint8_t*>(sg.in.p);
+        G.in_ps = sg.in.ps;
+        G.in_l = sg.in.l;
+        G.w1 = sg.c1->wx6;
+        G.b1 = sg.c1->bias;
+        G.w2 = sg.c2->wx6;
+        G.b2 = sg.c2->bias;
+        G.out = sg.out.p;
+        G.out_ps = sg.out.ps;
+        G.out_l = sg.out.l;
+        G.out_c = sg.out.c;
+        G.out_off = sg.out.off;
+        G.out_f32 = sg.out.f32 ? 1 : 0;
+        G.cout2 = sg.c2->cout;
+        G.relu2 = sg.relu2 ? 1 : 0;
+        G.N = sg.N;
+        G.H = sg.H;
+        G.W = sg.W;
+        G.npix = sg.N * sg.H * sg.W;
+        npix_all += G.npix;
+        flops += 2.0 * G.npix * ((double)sg.c1->cout * sg.c1->K + (double)sg.c2->cout * sg.c2->K);
+    }
+    ProfEntry pe;
+    h->prof_begin(pe, "conv1x1", flops, 0);
+    if (h->detail)
+        pe.detail = "layer/" + segs[0].c1->name + ">" + segs[0].c2->name + "/chain/g" + std::to_string(a.ngroups) + "/n" +
+                    std::to_string(npix_all);
+    launch_conv1x1_chain_x6(a, h->stream);
+    h->prof_end(pe);
 }
 
 // Zero the padding units of X6P buffers (cg groups each) for an N x H x W geometry.  The convs
@@ -1051,28 +1120,44 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
     layer("conv5_3_CPM_L1", "conv5_3_CPM_L2", [&](size_t i) { return t_(i, 1, 0); },
           [&](size_t i) { return t_(i, 0, 0); }, [&](size_t i) { return t_(i, 1, 16); },
           [&](size_t i) { return t_(i, 0, 16); }, true, true);
-    layer("conv5_4_CPM_L1", "conv5_4_CPM_L2", [&](size_t i) { return t_(i, 0, 0); }, [&](size_t i) { return u_(i, 0); },
-          [&](size_t i) { return t_(i, 0, 16); }, [&](size_t i) { return u_(i, 64); }, true, true);
-    layer("conv5_5_CPM_L1", "conv5_5_CPM_L2", [&](size_t i) { return u_(i, 0); }, [&](size_t i) { return s_(i, 1, 0); },
-          [&](size_t i) { return u_(i, 64); }, [&](size_t i) { return s_(i, 1, 5); }, false, false);
+    // 1x1 pairs of both branches and every segment: L1 then L2 of each segment
+    auto chain = [&](const std::string& a1, const std::string& a2, const std::string& b1, const std::string& b2,
+                     const std::function<ChainSeg(size_t, int, DevConv*, DevConv*)>& mk) {
+        DevConv *ca1 = find_conv(h, net, a1), *ca2 = find_conv(h, net, a2);
+        DevConv *cb1 = find_conv(h, net, b1), *cb2 = find_conv(h, net, b2);
+        std::vector<ChainSeg> cs;
+        for (size_t i = 0; i < ns; ++i) {
+            cs.push_back(mk(i, 0, ca1, ca2));
+            cs.push_back(mk(i, 1, cb1, cb2));
+        }
+        run_chain_x6(h, cs);
+    };
+    chain("conv5_4_CPM_L1", "conv5_5_CPM_L1", "conv5_4_CPM_L2", "conv5_5_CPM_L2",
+          [&](size_t i, int br, DevConv* c1, DevConv* c2) {
+              return ChainSeg{c1, c2, bs[i].N, bs[i].hl, bs[i].wl, t_(i, 0, br ? 16 : 0), u_(i, br ? 64 : 0),
+                              s_(i, 1, br ? 5 : 0), false};
+          });
     int cur = 1;
     for (int st = 2; st <= 6; ++st) {
         const std::string sf = "_stage" + std::to_string(st);
         layer("Mconv1" + sf + "_L1+L2", "", [&](size_t i) { return s_(i, cur, 0); },
               [&](size_t i) { return t_(i, 0, 0); }, none, none, true, false);
         int t = 0;
-        for (int k = 2; k <= 6; ++k) {
+        for (int k = 2; k <= 5; ++k) {
             const std::string nm = "Mconv" + std::to_string(k) + sf;
             layer(nm + "_L1", nm + "_L2", [&](size_t i) { return t_(i, t, 0); },
                   [&](size_t i) { return t_(i, t ^ 1, 0); }, [&](size_t i) { return t_(i, t, 16); },
                   [&](size_t i) { return t_(i, t ^ 1, 16); }, true, true);
             t ^= 1;
         }
-        // Mconv7: no ReLU, except Mconv7_stage6_L2 (no_relu list quirk, src/model.py:30-33)
-        layer("Mconv7" + sf + "_L1", "Mconv7" + sf + "_L2", [&](size_t i) { return t_(i, t, 0); },
-              [&](size_t i) { return st == 6 ? f32act(bs[i].O, 185, 0) : s_(i, cur ^ 1, 0); },
-              [&](size_t i) { return t_(i, t, 16); },
-              [&](size_t i) { return st == 6 ? f32act(bs[i].O, 185, 38) : s_(i, cur ^ 1, 5); }, false, st == 6);
+        // Mconv6 -> Mconv7; Mconv7: no ReLU, except Mconv7_stage6_L2 (no_relu list quirk,
+        // src/model.py:30-33)
+        chain("Mconv6" + sf + "_L1", "Mconv7" + sf + "_L1", "Mconv6" + sf + "_L2", "Mconv7" + sf + "_L2",
+              [&](size_t i, int br, DevConv* c1, DevConv* c2) {
+                  const XAct o = st == 6 ? f32act(bs[i].O, 185, br ? 38 : 0) : s_(i, cur ^ 1, br ? 5 : 0);
+                  return ChainSeg{c1, c2, bs[i].N, bs[i].hl, bs[i].wl, t_(i, t, br ? 16 : 0), t_(i, t ^ 1, br ? 16 : 0), o,
+                                  br == 1 && st == 6};
+              });
         cur ^= 1;
     }
     std::vector<float*> outs;
@@ -1120,21 +1205,30 @@ static std::vector<float*> hand_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
         for (size_t i = 0; i < ns; ++i) cs.push_back(ConvSeg{c, bs[i].N, bs[i].hl, bs[i].wl, in(i), out(i), XAct{}, relu});
         run_conv_x6_segs(h, cs);
     };
+    auto chain = [&](const std::string& n1, const std::string& n2, const std::function<ChainSeg(size_t, DevConv*, DevConv*)>& mk) {
+        DevConv *c1 = find_conv(h, net, n1), *c2 = find_conv(h, net, n2);
+        std::vector<ChainSeg> cs;
+        for (size_t i = 0; i < ns; ++i) cs.push_back(mk(i, c1, c2));
+        run_chain_x6(h, cs);
+    };
     run_trunk_x6(h, net, segs, last, dup);
-    layer("conv6_1_CPM", [&](size_t i) { return s_(i, 0, 3); }, u_, true);
-    layer("conv6_2_CPM", u_, [&](size_t i) { return s_(i, 1, 0); }, false);
+    chain("conv6_1_CPM", "conv6_2_CPM", [&](size_t i, DevConv* c1, DevConv* c2) {
+        return ChainSeg{c1, c2, bs[i].N, bs[i].hl, bs[i].wl, s_(i, 0, 3), u_(i), s_(i, 1, 0), false};
+    });
     int cur = 1;
     for (int st = 2; st <= 6; ++st) {
         const std::string sf = "_stage" + std::to_string(st);
         layer("Mconv1" + sf, [&](size_t i) { return s_(i, cur, 0); }, [&](size_t i) { return t_(i, 0); }, true);
         int t = 0;
-        for (int k = 2; k <= 6; ++k) {
+        for (int k = 2; k <= 5; ++k) {
             layer("Mconv" + std::to_string(k) + sf, [&](size_t i) { return t_(i, t); },
                   [&](size_t i) { return t_(i, t ^ 1); }, true);
             t ^= 1;
         }
-        layer("Mconv7" + sf, [&](size_t i) { return t_(i, t); },
-              [&](size_t i) { return st == 6 ? f32act(bs[i].O, 150, 0) : s_(i, cur ^ 1, 0); }, false);
+        chain("Mconv6" + sf, "Mconv7" + sf, [&](size_t i, DevConv* c1, DevConv* c2) {
+            const XAct o = st == 6 ? f32act(bs[i].O, 150, 0) : s_(i, cur ^ 1, 0);
+            return ChainSeg{c1, c2, bs[i].N, bs[i].hl, bs[i].wl, t_(i, t), t_(i, t ^ 1), o, false};
+        });
         cur ^= 1;
     }
     std::vector<float*> outs;

@@ -47,6 +47,8 @@ void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t o
 // conv1_2 (64 -> 64, 3x3 pad 1) + MaxPool2d(2, 2) from an 8-group X6 tensor, input window in LDS
 void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int W, const uint8_t* wt,
                               const float* bias, uint8_t* out, uint32_t ops, hipStream_t st);
+// conv1x1_chain.hip: two chained 1x1 convs (CPM stage ends) in one launch, 64-pixel tiles
+void launch_conv1x1_chain_x6(const X6ChainArgs& a, hipStream_t st);
 // conv_win.hip: the 7x7 / 3x3 convs with the im2col operand from an LDS window of the padded X6P
 // input (pair-order weights: x6_pack_weights_pairs); 128 x 256 tiles, data parallel
 // (sk_grid == tiles) or stream-K

@@ -262,3 +262,26 @@ def test_hand_pyramid_vs_oracle(native):
     for x, a in zip(xs, pyr):
         r = network.hand_forward(torch.from_numpy(x), sd).numpy()
         np.testing.assert_allclose(a, r, rtol=2e-4, atol=2e-4 * float(np.abs(r).max()))
+
+
+@pytest.mark.parametrize("kind,shape,exact", [("body", (32, 3, 184, 328), True), ("body", (2, 3, 72, 104), False),
+                                              ("hand", (1, 3, 88, 88), False), ("hand", (120, 3, 184, 184), False)],
+                         ids=["bench32", "body72x104", "hand88", "hand120"])
+def test_fused_1x1_chain(native, kind, shape, exact):
+    """The closing 1x1 pair of every CPM stage in one launch (conv1x1_chain_x6, default) against
+    two conv_x6 launches through an HBM intermediate (OPOSE_FUSE_1X1=0): the same piece products
+    in the same order, so on the bench's batch -- where conv_x6 runs both convs on whole tiles --
+    the network outputs are bit-identical; at small sizes conv_x6 splits k (stream-K) and the bar
+    is fp32 summation-order noise."""
+    from src.model import bodypose_model, handpose_model
+    cls = bodypose_model if kind == "body" else handpose_model
+    x = np.random.default_rng(14).random(shape, dtype=np.float32) - np.float32(0.5)
+    fused = _model_outputs(cls, kind, x, {"OPOSE_FUSE_1X1": "1"})
+    split = _model_outputs(cls, kind, x, {"OPOSE_FUSE_1X1": "0"})
+    for a, r in zip(fused, split):
+        if exact:
+            assert np.array_equal(a, r), kind
+        else:
+            tol = 2e-4 * np.abs(r).max() + 2e-4 * np.abs(r)
+            assert (np.abs(a - r) <= tol).all()
+            assert np.abs(a - r).max() <= 5e-5 * np.abs(r).max()
