@@ -47,7 +47,8 @@ PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA peak (no sparsity)
 # (algorithmic) FLOP/s is the bf16 peak / 6.
 X6 = os.environ.get("OPOSE_CONV", "x6") != "f32"
 PEAK_CONV_TFLOPS = PEAK_BF16_TFLOPS / 6 if X6 else PEAK_FP32_TFLOPS
-CONV_KERNEL = "conv_x6" if X6 else "conv_igemm_f32"
+# the 7x7 CPM convs of the bench's batch run on the LDS-window kernel (conv_win.hip)
+CONV_KERNEL = "conv_win_x6" if X6 else "conv_igemm_f32"
 
 
 def parse():
@@ -94,9 +95,9 @@ def pmc_traffic():
         rec = json.load(open(path))
     except (OSError, ValueError):
         return None
-    # the 7x7 class runs as one or two kernel instantiations (conv_x6<MT, PT, false, 7, MODE>,
-    # 128x256 for the grouped 128-channel convs, 256x128 for Mconv1); dispatch-weighted mean
-    tag = ", false, 7," if X6 else ", true, 7, 0>"
+    # the 7x7 class: conv_win_x6<128, 256, 7, WMAX, stages> (one instantiation at the bench's
+    # shape); dispatch-weighted mean over whatever 7x7 instantiations the profile holds
+    tag = "<128, 256, 7," if X6 else ", true, 7, 0>"
     num = den = 0.0
     for name, v in rec.items():
         if CONV_KERNEL + "<" in name and tag in name and "hbm_bytes_per_launch" in v:

@@ -151,6 +151,27 @@ def main():
     out["C5_status_nonzero"] = int((st != 0).sum())
     out["C5_mean_peaks_people"] = rec5.view(torch.int32)[:, 1:3].float().mean(0).cpu().tolist()
 
+    # the same C5 work with the four scales' networks in lockstep (OPOSE_LOCKSTEP=2: one conv
+    # launch per layer for all scales, as Hand() runs; not the default for Body because the
+    # scale-sharded split would then no longer reproduce Body(frame) bit for bit)
+    os.environ["OPOSE_LOCKSTEP"] = "2"
+    try:
+        body5l = Body(seeded_state_dict("body", 0, out_scale=cal), scale_search=(0.5, 1.0, 1.5, 2.0))
+    finally:
+        del os.environ["OPOSE_LOCKSTEP"]
+
+    def step5l():
+        body5l.infer_records(f5, rec5)
+        body5l.handle.synchronize()
+    ms = timed(step5l, 5, warm=1)
+    out["C5_lockstep_frames_per_s_per_gpu"] = B / (ms * 1e-3)
+
+    def one5l():
+        body5l.infer_records(f5[:1].contiguous(), rec5[:1])
+        body5l.handle.synchronize()
+    out["C5_lockstep_single_frame_latency_ms"] = timed(one5l, 10, warm=2)
+    del body5l
+
     # C5 single-frame latency: all four scales on one GPU vs the scale-sharded split
     # (src.dist.body_scale_sharded): per-scale network time and the multi-scale post on the
     # gathered low-res maps, measured here; the sharded latency is max over ranks of its scales'
