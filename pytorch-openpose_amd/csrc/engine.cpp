@@ -1375,8 +1375,10 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
         // one scale, a true upsampling resize (the reference's 368-row frames at scale 0.5): the
         // resize runs inside the NMS tiles (post.hip gauss_nms_resize) and tiles whose sources
         // cannot produce a peak are dropped, so no full-resolution map is written or read.
-        // bytes: the x8 heat channels the tiles read (the kernel's algorithmic traffic)
-        h->prof_begin(pe, "gauss_nms_resize", 0, (double)N * 18 * 4.0 * gs[0].Hs * gs[0].Ws);
+        // float64-VALU bound: flops = the reference filter's 2 x 37 float64 operations per
+        // full-resolution part-map pixel (bench.py GAUSS_OPS_PER_PIXEL); bytes: the x8 heat
+        // channels the tiles read
+        h->prof_begin(pe, "gauss_nms_resize", 74.0 * N * 18 * (double)H * W, (double)N * 18 * 4.0 * gs[0].Hs * gs[0].Ws);
         launch_gauss_nms_resize(S.mid[0], 56, 38, 18, N, gs[0].Hs, gs[0].Ws, H, W, gs[0].up_sy, gs[0].up_sx, p.thre1,
                                 cap, cnt, list, lscore, h->stream);
         h->prof_end(pe);
