@@ -2398,37 +2398,16 @@ int opose_hand_infer_crops(opose_t* h, const uint8_t* const* crops, const int* s
                                                hipMemcpyHostToDevice, h->stream));
         }
         // all crops of a scale form one batch; with the split-bf16 path all scales run in lockstep
-        // (one conv launch per layer for every crop and scale)
+        // (one conv launch per layer for every crop and scale).  Batches are cut so that the
+        // largest activation (64 channels at the largest scale's full resolution, X6: 3 x 128 B
+        // per pixel) stays below the 2 GiB the conv kernels address with 32-bit offsets.
         const bool lockstep = h->x6 && h->lockstep && ns > 1;
         if (lockstep && !h->loaded[OPOSE_NET_HAND]) throw std::runtime_error("hand weights not loaded");
-        std::vector<NetSeg> segs;
-        for (int s = 0; s < ns; ++s) {
-            const ScaleGeom& g0 = gs[0][s];
-            float* x = h->ws[lockstep ? s : h->slot].x.ensure<float>((size_t)n * 3 * g0.Hp * g0.Wp, h->stream);
-            ProfEntry pe;
-            h->prof_begin(pe, "preprocess", 0, 0);
-            for (int i = 0; i < n; ++i) {
-                const ScaleGeom& g = gs[i][s];
-                const uint8_t* src = buf ? buf + off[i] : crops[i];
-                launch_preprocess(src, (int64_t)(off[i + 1] - off[i]), row_strides[i], 1, sizes[i], sizes[i], g.Hs,
-                                  g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp, g.Wp, (float)p.pad_value / 256.f - 0.5f,
-                                  x + (size_t)i * 3 * g.Hp * g.Wp, h->stream);
-            }
-            h->prof_end(pe);
-            if (lockstep) {
-                segs.push_back(NetSeg{x, n, g0.Hp, g0.Wp, s});
-                continue;
-            }
-            float* Sb = hand_net(h, x, n, g0.Hp, g0.Wp);
-            upsample_to_mid(h, s, Sb, 150, n, g0, 21);
-        }
-        if (lockstep) {
-            const std::vector<float*> outs = hand_net_x6(h, segs);
-            for (int s = 0; s < ns; ++s) upsample_to_mid(h, s, outs[s], 150, n, gs[0][s], 21);
-        }
-        (void)base;
+        size_t maxpix = 0;
+        for (int s = 0; s < ns; ++s) maxpix = std::max(maxpix, (size_t)gs[0][s].Hp * gs[0][s].Wp);
+        const int chunk = (int)std::max<size_t>(1, (((size_t)1 << 31) - 1) / (3 * 128 * maxpix));
         // size every per-crop buffer for the largest crop / all crops up front: a reallocation
-        // inside the loop would drop the results of the crops already done
+        // after the first batch would drop the results of the crops already done
         const int wmax = *std::max_element(sizes, sizes + n);
         h->avg.ensure<double>((size_t)21 * wmax * wmax, h->stream);
         h->hlab.ensure<int>((size_t)21 * wmax * wmax, h->stream);
@@ -2437,8 +2416,37 @@ int opose_hand_infer_crops(opose_t* h, const uint8_t* const* crops, const int* s
             h->hpeaks.ensure<double>((size_t)n * 21 * 3, h->stream);
             h->hfound.ensure<int>((size_t)n * 21, h->stream);
         }
-        for (int i = 0; i < n; ++i)
-            hand_post_common(h, 1, sizes[i], sizes[i], gs[i], p, peaks, found, flags & OPOSE_OUT_DEVICE, i, i);
+        for (int c0 = 0; c0 < n; c0 += chunk) {
+            const int nc = std::min(chunk, n - c0);
+            std::vector<NetSeg> segs;
+            for (int s = 0; s < ns; ++s) {
+                const ScaleGeom& g0 = gs[0][s];
+                float* x = h->ws[lockstep ? s : h->slot].x.ensure<float>((size_t)nc * 3 * g0.Hp * g0.Wp, h->stream);
+                ProfEntry pe;
+                h->prof_begin(pe, "preprocess", 0, 0);
+                for (int i = c0; i < c0 + nc; ++i) {
+                    const ScaleGeom& g = gs[i][s];
+                    const uint8_t* src = buf ? buf + off[i] : crops[i];
+                    launch_preprocess(src, (int64_t)(off[i + 1] - off[i]), row_strides[i], 1, sizes[i], sizes[i], g.Hs,
+                                      g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp, g.Wp, (float)p.pad_value / 256.f - 0.5f,
+                                      x + (size_t)(i - c0) * 3 * g.Hp * g.Wp, h->stream);
+                }
+                h->prof_end(pe);
+                if (lockstep) {
+                    segs.push_back(NetSeg{x, nc, g0.Hp, g0.Wp, s});
+                    continue;
+                }
+                float* Sb = hand_net(h, x, nc, g0.Hp, g0.Wp);
+                upsample_to_mid(h, s, Sb, 150, nc, g0, 21);
+            }
+            if (lockstep) {
+                const std::vector<float*> outs = hand_net_x6(h, segs);
+                for (int s = 0; s < ns; ++s) upsample_to_mid(h, s, outs[s], 150, nc, gs[0][s], 21);
+            }
+            for (int i = c0; i < c0 + nc; ++i)
+                hand_post_common(h, 1, sizes[i], sizes[i], gs[i], p, peaks, found, flags & OPOSE_OUT_DEVICE, i - c0, i);
+        }
+        (void)base;
         hand_finish(h, n, peaks, found, flags & OPOSE_OUT_DEVICE);
     });
     return OPOSE_OK;

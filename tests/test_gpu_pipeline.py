@@ -133,3 +133,17 @@ def test_extract_motion_data_device_ingest_equals_host(nets):
         host = extract_motion_data(iter(video), body, hand, recpoint=rec, mode=mode, batch=3, device=False)
         assert dev.shape == host.shape == (11, 60 if mode == "bodyhand" else 18, 3)
         assert np.array_equal(dev, host), mode
+
+
+def test_hand_batch_crops_beyond_one_launch(nets):
+    """More crops than one network launch holds (at the 736-pixel scale ten crops fill the 2 GiB
+    the conv kernels address): the batch is cut into launches of at most ten, every crop's
+    result equals its single-crop Hand()."""
+    _, hsd, _, Hand = nets
+    hand = Hand(hsd)
+    rng = np.random.default_rng(43)
+    crops = [rng.integers(0, 256, (64, 64, 3), dtype=np.uint8) for _ in range(12)]
+    batch = hand.batch_crops(crops)
+    assert len(batch) == 12
+    for c, b in zip(crops, batch):
+        np.testing.assert_allclose(b, hand(c), rtol=1e-4, atol=1e-5)
