@@ -38,17 +38,22 @@ def gather_records(rec: torch.Tensor, n_frames: int, world: int, group=None) -> 
     if rec.shape[0] < cap:
         pad = torch.zeros((cap - rec.shape[0], rb), dtype=rec.dtype, device=rec.device)
         rec = torch.cat([rec, pad], 0)
-    backend = dist.get_backend(group)
-    if backend == "nccl":
-        out = torch.empty((world * cap, rb), dtype=rec.dtype, device=rec.device)
-        dist.all_gather_into_tensor(out, rec.contiguous(), group=group)
-        parts = list(out.view(world, cap, rb))
-    else:  # gloo: through host memory
-        host = rec.cpu()
-        parts = [torch.empty_like(host) for _ in range(world)]
-        dist.all_gather(parts, host.contiguous(), group=group)
-        parts = [p.to(rec.device) for p in parts]
+    parts = all_gather_padded(rec, world, group)
     return torch.cat([p[:hi - lo] for p, (lo, hi) in zip(parts, per)], 0)
+
+
+def all_gather_padded(rec: torch.Tensor, world: int, group=None):
+    """The collective of gather_records: every rank's [cap, record_bytes] block, rank order.
+    RCCL ('nccl'): one all_gather_into_tensor on the device tensors; gloo: through host memory."""
+    rb = rec.shape[1]
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty((world * rec.shape[0], rb), dtype=rec.dtype, device=rec.device)
+        dist.all_gather_into_tensor(out, rec.contiguous(), group=group)
+        return list(out.view(world, rec.shape[0], rb))
+    host = rec.cpu()
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host.contiguous(), group=group)
+    return [p.to(rec.device) for p in parts]
 
 
 # ---------------------------------------------------------------- single-frame scale sharding
