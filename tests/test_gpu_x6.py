@@ -285,3 +285,19 @@ def test_fused_1x1_chain(native, kind, shape, exact):
             tol = 2e-4 * np.abs(r).max() + 2e-4 * np.abs(r)
             assert (np.abs(a - r) <= tol).all()
             assert np.abs(a - r).max() <= 5e-5 * np.abs(r).max()
+
+
+@pytest.mark.parametrize("crops", [1, 2])
+def test_hand_pyramid_window_vs_im2col(native, crops):
+    """A 368 crop's pyramid in lockstep on the window kernel (stream-K 128 x 256 window tiles over
+    the four scales' groups) against conv_x6 over the im2col stream (OPOSE_CONV7_WIN=0):
+    pair-order vs group-tap-order summation, the network tolerance and a maximum deviation below
+    5e-5 of the map's range."""
+    rng = np.random.default_rng(19)
+    xs = [rng.random((crops, 3, s, s), dtype=np.float32) - np.float32(0.5) for s in (184, 368, 552, 736)]
+    win = _hand_model({"OPOSE_CONV7_WIN": "1"}).forward_pyramid(xs)
+    ref = _hand_model({"OPOSE_CONV7_WIN": "0"}).forward_pyramid(xs)
+    for a, r in zip(win, ref):
+        tol = 2e-4 * np.abs(r).max() + 2e-4 * np.abs(r)
+        assert (np.abs(a - r) <= tol).all()
+        assert np.abs(a - r).max() <= 5e-5 * np.abs(r).max()
