@@ -153,7 +153,7 @@ def main():
 
     # the same C5 work with the four scales' networks in lockstep (OPOSE_LOCKSTEP=2: one conv
     # launch per layer for all scales, as Hand() runs; not the default for Body because the
-    # scale-sharded split would then no longer reproduce Body(frame) bit for bit, DESIGN §6)
+    # scale-sharded split would then no longer reproduce Body(frame) bit for bit, DESIGN §4.3)
     os.environ["OPOSE_LOCKSTEP"] = "2"
     try:
         body5l = Body(seeded_state_dict("body", 0, out_scale=cal), scale_search=(0.5, 1.0, 1.5, 2.0))

@@ -2,7 +2,7 @@
 
 * No VOP3P packed-FP32 arithmetic (`v_pk_add_f32`, `v_pk_mul_f32`, `v_pk_fma_f32`) anywhere in
   libopose.so: compiler-generated packed-FP32 code gave wrong low-element results when its kernel
-  ran beside the pipelined network stream's kernels (DESIGN §4.3), so every kernel is built with
+  ran beside the pipelined network stream's kernels (DESIGN §4.6), so every kernel is built with
   `-target-feature -packed-fp32-ops` (pytorch-openpose_amd/Makefile NOPK).  A flag or toolchain
   change that brings them back fails here instead of in a rare pipelined frame.
 * The split-bf16 convolution is on the matrix cores: the conv code object holds
