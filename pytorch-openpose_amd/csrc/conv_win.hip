@@ -63,6 +63,8 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     const int nK = a.nK;
     const int wm0 = (wave % NWM) * WM;
     const int wp0 = (wave / NWM) * WP;
+    // two waves per SIMD: the younger half issues first when both are ready (guide T5, static form)
+    if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
     // stream-K range of this workgroup over (tile, chunk), XCD-contiguous (guide T1); a grid of
     // one workgroup per tile is the data-parallel case.  Pieces run from the range end backwards.

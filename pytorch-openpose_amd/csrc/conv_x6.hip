@@ -449,8 +449,26 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     }
 }
 
-// Stream-K fixup: grid (tiles, MT*PT/256/8); each thread finishes 4 consecutive channels (half
-// a group) of one pixel of a shared tile: partial slabs summed in k order (deterministic).
+// whole X6 unit (8 channels of one pixel): three 16-byte piece stores
+__device__ __forceinline__ void store8_x6(uint8_t* unit, uint32_t ps, const float (&v)[8]) {
+    uint32_t h[3][8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) split3(v[t], h[0][t], h[1][t], h[2][t]);
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+        uint4 w;
+        w.x = h[pc][0] | (h[pc][1] << 16);
+        w.y = h[pc][2] | (h[pc][3] << 16);
+        w.z = h[pc][4] | (h[pc][5] << 16);
+        w.w = h[pc][6] | (h[pc][7] << 16);
+        *reinterpret_cast<uint4*>(unit + (size_t)pc * ps) = w;
+    }
+}
+
+// Stream-K fixup: grid (tiles, MT*PT/8/256); each thread finishes one X6 unit (8 channels of one
+// pixel) of a shared tile: partial slabs summed in k order (deterministic).  Pixels run fastest
+// across the lanes, so every slab load is a coalesced 256-byte row segment and every store a
+// whole 16-byte unit; two slabs' loads are in flight per round trip.
 template <int MT, int PT>
 __global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
     const int nM = a.Mpad / MT;
@@ -462,32 +480,47 @@ __global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
     const int w0 = (int)(((x0 + 1) * Gw - 1) / I);
     const int w1 = (int)(((x0 + nK) * Gw - 1) / I);
     if (w0 == w1) return;
-    const X6Group& G = a.g[x6_group_of(a, tile)];
+    const X6Group G = a.g[x6_group_of(a, tile)];
     const int mt = (tile - G.t0) % nM;
     const int pt = (tile - G.t0) / nM;
     const int HW = G.H * G.W;
-    // thread -> (quad of channels, pixel); pixels fastest so slab reads stay coalesced
-    const int e = blockIdx.y * 256 + threadIdx.x;  // < MT/4 * PT
-    const int pl = e % PT, mq = e / PT;
-    const int ml0 = mq * 4;
-    const int mg = mt * MT + ml0;  // first channel of the quad
+    const int e = blockIdx.y * 256 + threadIdx.x;  // < MT/8 * PT
+    const int pl = e % PT, ml0 = (e / PT) * 8;
+    const int mg = mt * MT + ml0;  // first channel of the unit
     const int p = pt * PT + pl;
     if (p >= G.npix) return;
     const int cout8 = (G.cout + 7) & ~7;
     if (mg >= (G.out_f32 ? G.cout : cout8)) return;
-    float v[4];
-    for (int w = w0; w <= w1; ++w) {
+    auto slab = [&](int w) __attribute__((always_inline)) {
         const long long lo_w = (long long)w * I / Gw;
         const int slot = (lo_w / nK == tile) ? 2 * w : 2 * w + 1;
-        const float* s = a.partial + (size_t)slot * (MT * PT) + pl;
+        return a.partial + (size_t)slot * (MT * PT) + (size_t)ml0 * PT + pl;
+    };
+    float v[8];
+    {
+        const float* s = slab(w0);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const float x = s[(size_t)(ml0 + t) * PT];
-            v[t] = (w == w0) ? x : v[t] + x;
+        for (int t = 0; t < 8; ++t) v[t] = s[(size_t)t * PT];
+    }
+    int w = w0 + 1;
+    for (; w < w1; w += 2) {
+        const float *s0 = slab(w), *s1 = slab(w + 1);
+        float x0v[8], x1v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            x0v[t] = s0[(size_t)t * PT];
+            x1v[t] = s1[(size_t)t * PT];
         }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = (v[t] + x0v[t]) + x1v[t];
+    }
+    if (w == w1) {
+        const float* s = slab(w);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] += s[(size_t)t * PT];
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 8; ++t) {
         const int m = mg + t;
         v[t] += m < G.cout ? G.bias[m] : 0.f;
         if (G.relu) v[t] = fmaxf(v[t], 0.f);
@@ -497,16 +530,14 @@ __global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
     if (G.out_f32) {
         float* ob = static_cast<float*>(G.out) + ((size_t)n * G.out_c + G.out_off) * HW + rem;
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 8; ++t)
             if (mg + t < G.cout) ob[(size_t)(mg + t) * HW] = v[t];
         return;
     }
-    const int grp = mg >> 3, half = (mg >> 2) & 1;
+    const int grp = mg >> 3;
     const int y = rem / G.W, x = rem - y * G.W;
-    store4_x6(static_cast<uint8_t*>(G.out) + (size_t)x6_unit(G.out_l, n, grp, y, x) * 16 + half * 8, G.out_ps, v);
-    if (G.out2)
-        store4_x6(static_cast<uint8_t*>(G.out2) + (size_t)x6_unit(G.out2_l, n, grp, y, x) * 16 + half * 8, G.out2_ps,
-                  v);
+    store8_x6(static_cast<uint8_t*>(G.out) + (size_t)x6_unit(G.out_l, n, grp, y, x) * 16, G.out_ps, v);
+    if (G.out2) store8_x6(static_cast<uint8_t*>(G.out2) + (size_t)x6_unit(G.out2_l, n, grp, y, x) * 16, G.out2_ps, v);
 }
 
 static int grid_for(size_t total) {
@@ -741,12 +772,12 @@ static void launch_x6_tile(const X6Args& a0, hipStream_t st) {
     else
         hipLaunchKernelGGL((conv_x6<MT, PT, false, 0>), dim3(a.sk_grid), blk, 0, st, a);
     if (a.sk_grid != a.tiles)
-        hipLaunchKernelGGL((conv_x6_fixup<MT, PT>), dim3(a.tiles, MT * PT / 4 / 256), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((conv_x6_fixup<MT, PT>), dim3(a.tiles, MT * PT / 8 / 256), dim3(256), 0, st, a);
 }
 
 void launch_conv_x6_fixup(const X6Args& a, int mt, int pt, hipStream_t st) {
     if (mt != 128 || pt != 256) throw std::invalid_argument("conv_x6_fixup: tile");
-    hipLaunchKernelGGL((conv_x6_fixup<128, 256>), dim3(a.tiles, 128 * 256 / 4 / 256), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_x6_fixup<128, 256>), dim3(a.tiles, 128 * 256 / 8 / 256), dim3(256), 0, st, a);
 }
 
 void launch_conv_x6(const X6Args& a, int mt, int pt, hipStream_t st) {

@@ -221,6 +221,12 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_WIN_SK");
         return e && e[0] == '0';
     }();
+    // multi-frame segments whose windows overflow the LDS run as one segment per frame on the
+    // window kernel (run_conv_x6_segs); OPOSE_SPLIT_FRAMES=0: conv_x6 for such launches (A/B)
+    bool split_frames = [] {
+        const char* e = getenv("OPOSE_SPLIT_FRAMES");
+        return !(e && e[0] == '0');
+    }();
     // conv1_2 + pool by conv3_pool_win_x6 (input window in LDS; OPOSE_CONV12_WIN=0: conv_x6's
     // pooled 64 x 128 tile over the im2col stream)
     bool win12 = [] {
@@ -697,8 +703,59 @@ struct ConvSeg {
 // branch pair of a stage and the scales of a pyramid share one grid (X6Args groups).
 // pool: MaxPool2d(2, 2) (src/model.py:10-13, floor mode) fused into the epilogue; out is then the
 // pooled [N][(H/2)(W/2)] X6 tensor (conv outputs the floor mode drops are never computed)
-static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, bool pool = false) {
+static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, bool pool = false);
+
+// frame n of an activation (N frames of H x W) as a one-frame activation of the same buffer
+static XAct frame_view(const XAct& a, int n, int H, int W) {
+    XAct v = a;
+    if (!a.p) return v;
+    if (a.f32) v.p = static_cast<float*>(a.p) + (size_t)n * a.c * H * W;
+    else v.l.o0 = a.l.o0 + (uint32_t)n * a.l.fs;
+    return v;
+}
+
+// A multi-frame 7x7 segment on a padded input whose 256-pixel tiles straddle two frames with a window
+// larger than the LDS holds (a crop batch's largest pyramid scale: 2 x 92 x 92) would send
+// the whole launch to conv_x6: run such segments as one segment per frame (frame views of the
+// same buffers), whose windows fit, when the launch has group slots for them.
+static bool split_frames_for_win(const opose_ctx* h, const std::vector<ConvSeg>& segs, bool pool,
+                                 std::vector<ConvSeg>& out) {
+    if (!h->win7 || pool || segs.size() > (size_t)kX6Groups) return false;
+    size_t groups = 0;
+    bool any = false;
+    for (const ConvSeg& sg : segs) {
+        // 7x7 only: at 3x3 the per-crop windows measured slower than conv_x6 on the whole batch
+        // (conv3_x of two 368 crops 0.65 vs 0.62 ms), at 7x7 faster (0.24 vs 0.27 ms + fixups)
+        if (!sg.c->wx6p || !sg.in.padded || sg.c->ks != 7) return false;
+        if (conv_win_fits(sg.N, sg.H, sg.W, sg.c->ks)) {
+            ++groups;
+        } else if (sg.N > 1 && conv_win_fits(1, sg.H, sg.W, sg.c->ks)) {
+            groups += sg.N;
+            any = true;
+        } else {
+            return false;
+        }
+    }
+    if (!any || groups > (size_t)kX6Groups) return false;
+    out.clear();
+    for (const ConvSeg& sg : segs) {
+        if (conv_win_fits(sg.N, sg.H, sg.W, sg.c->ks)) {
+            out.push_back(sg);
+            continue;
+        }
+        for (int n = 0; n < sg.N; ++n)
+            out.push_back(ConvSeg{sg.c, 1, sg.H, sg.W, frame_view(sg.in, n, sg.H, sg.W),
+                                  frame_view(sg.out, n, sg.H, sg.W), frame_view(sg.dup, n, sg.H, sg.W), sg.relu});
+    }
+    return true;
+}
+
+static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, bool pool) {
     if (segs.empty()) return;
+    {
+        std::vector<ConvSeg> per_frame;
+        if (h->split_frames && split_frames_for_win(h, segs, pool, per_frame)) return run_conv_x6_segs(h, per_frame, pool);
+    }
     if (segs.size() > (size_t)kX6Groups) {  // more scales x branches than one launch holds
         for (size_t i = 0; i < segs.size(); i += kX6Groups)
             run_conv_x6_segs(h, std::vector<ConvSeg>(segs.begin() + i, segs.begin() + std::min(segs.size(), i + kX6Groups)),

@@ -251,6 +251,23 @@ def test_hand_pyramid_lockstep_vs_per_scale(native, crops, sizes, env):
         assert np.abs(a - r).max() <= 5e-5 * np.abs(r).max()
 
 
+@pytest.mark.parametrize("crops", [2, 3])
+def test_hand_crop_batch_per_frame_windows(native, crops):
+    """A crop batch's largest scale (N x 92 x 92 at the 7x7 layers): 256-pixel tiles that
+    straddle two crops need a window larger than the LDS, so the planner runs that segment as
+    one segment per crop (frame views of the same X6P buffers) on the window kernel (default) --
+    against the whole launch on conv_x6 (OPOSE_SPLIT_FRAMES=0): summation-order noise only
+    (3 smaller scales + one group per crop: up to 5 crops split)."""
+    rng = np.random.default_rng(19)
+    xs = [rng.random((crops, 3, s, s), dtype=np.float32) - np.float32(0.5) for s in (184, 368, 552, 736)]
+    a = _hand_model({}).forward_pyramid(xs)
+    r = _hand_model({"OPOSE_SPLIT_FRAMES": "0"}).forward_pyramid(xs)
+    for x, y in zip(a, r):
+        tol = 2e-4 * np.abs(y).max() + 2e-4 * np.abs(y)
+        assert (np.abs(x - y) <= tol).all()
+        assert np.abs(x - y).max() <= 5e-5 * np.abs(y).max()
+
+
 def test_hand_pyramid_vs_oracle(native):
     """The lockstep pyramid against the oracle network (oracle/network.py hand_forward, the
     reference's handpose_model restated) at small sizes: the network tolerance."""
