@@ -2283,7 +2283,7 @@ static void hand_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     h->prof_end(pe);
     h->prof_begin(pe, "hand_cc", 0, 0);
     void* ws = h->hsel.ensure<uint8_t>(hand_cc_workspace_bytes(NP), h->stream);
-    launch_hand_cc(avg, NP, H, W, lab, sums, cnt, pk, fd, ws, h->stream);
+    launch_hand_cc(avg, NP, H, W, lab, sums, cnt, pk, fd, ws, true, h->stream);
     h->prof_end(pe);
 }
 
@@ -2376,7 +2376,7 @@ static void batch_hand_post_common(opose_ctx* h, int N, int H, int W, const floa
     h->prof_end(pe);
     h->prof_begin(pe, "hand_cc", 0, 0);
     void* ws = h->hsel.ensure<uint8_t>(hand_cc_workspace_bytes(NP), h->stream);
-    launch_hand_cc(avg, NP, H, W, lab, sums, cnt, pk, fo, ws, h->stream);
+    launch_hand_cc(avg, NP, H, W, lab, sums, cnt, pk, fo, ws, false, h->stream);
     h->prof_end(pe);
     hand_finish(h, N, peaks, found, flags & OPOSE_OUT_DEVICE);
 }

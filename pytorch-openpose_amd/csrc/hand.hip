@@ -2,7 +2,8 @@
 //
 // Reference: hitmaxiang/pytorch-openpose src/hand.py:59-75 (per part):
 //   binary = gaussian_filter(map_ori, 3) > thre          (gauss_threshold in post.hip)
-//   label(binary, connectivity=2)                         => cc_union / cc_compress_sum
+//   label(binary, connectivity=2)                         => gauss_threshold (per 64x32 tile, in LDS)
+//                                                            + cc_border / cc_compress_sum
 //   best = argmax_i sum(map_ori[label == i]) + 1          => cc_compress_sum / hand_select_*
 //   map_ori[label != best] = 0; (y, x) = util.npmax(map_ori) (first row-major max)
 //
@@ -68,6 +69,38 @@ __global__ __launch_bounds__(256) void cc_union(int* __restrict__ lab, int H, in
             if (up && !ul) uf_union(L, i, u);
         }
         if (ur && !up) uf_union(L, i, u + 1);
+    }
+}
+
+// Seeds already labelled per 64 x 32 tile (gauss_threshold: every set pixel points at its
+// tile-local root): join components across tile edges.  One thread per pixel of a tile's top row
+// (links to the three pixels above it) and of its left column (links to the three pixels left of
+// it) -- every 8-adjacent pair of set pixels in different tiles is one of these.
+constexpr int kSeedTW = 64, kSeedTH = 32;
+
+__global__ __launch_bounds__(128) void cc_border(int* __restrict__ lab, int H, int W, int ntx) {
+    const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx, np = blockIdx.y;
+    const int x0 = tx * kSeedTW, y0 = ty * kSeedTH;
+    int* L = lab + (size_t)np * H * W;
+    const int t = threadIdx.x;
+    if (t < kSeedTW) {  // top row: (y0 - 1, x - 1 .. x + 1)
+        const int x = x0 + t, y = y0;
+        if (y0 == 0 || x >= W || y >= H) return;
+        const int i = y * W + x;
+        if (L[i] < 0) return;
+        for (int dx = -1; dx <= 1; ++dx) {
+            const int xx = x + dx;
+            if (xx >= 0 && xx < W && L[i - W + dx] >= 0) uf_union(L, i, i - W + dx);
+        }
+    } else if (t < kSeedTW + kSeedTH) {  // left column: (y - 1 .. y + 1, x0 - 1)
+        const int x = x0, y = y0 + t - kSeedTW;
+        if (x0 == 0 || y >= H) return;
+        const int i = y * W + x;
+        if (L[i] < 0) return;
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int yy = y + dy;
+            if (yy >= 0 && yy < H && L[i + dy * W - 1] >= 0) uf_union(L, i, i + dy * W - 1);
+        }
     }
 }
 
@@ -192,9 +225,15 @@ __global__ __launch_bounds__(64) void hand_select_reduce(const int* __restrict__
 size_t hand_cc_workspace_bytes(int NP) { return (size_t)NP * SEL_NB * (sizeof(double) + sizeof(int)) + NP * 4; }
 
 void launch_hand_cc(double* avg, int NP, int H, int W, int* lab, double* sums, const int* cnt, double* peaks,
-                    int* found, void* ws, hipStream_t st) {
+                    int* found, void* ws, bool tile_seeds, hipStream_t st) {
     dim3 grid((W + 255) / 256, H, NP);
-    hipLaunchKernelGGL(cc_union, grid, dim3(256), 0, st, lab, H, W);
+    if (tile_seeds) {
+        int ntx, nty;
+        gauss_threshold_tiles(H, W, &ntx, &nty);
+        hipLaunchKernelGGL(cc_border, dim3(ntx * nty, NP), dim3(128), 0, st, lab, H, W, ntx);
+    } else {
+        hipLaunchKernelGGL(cc_union, grid, dim3(256), 0, st, lab, H, W);
+    }
     OPOSE_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(double) * (size_t)NP * H * W, st));
     hipLaunchKernelGGL(cc_compress_sum, grid, dim3(256), 0, st, lab, avg, H, W, sums);
     double* part_v = static_cast<double*>(ws);

@@ -91,6 +91,7 @@ void launch_blur5_nms(const float* heat, int NP, int H, int W, double thre, int 
 void launch_blur5_seed(const float* heat, int NP, int H, int W, double thre, double* blurred, int* lab, int* cnt,
                        hipStream_t st);
 void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st);
+void gauss_threshold_tiles(int H, int W, int* ntx, int* nty);
 void launch_peaks_finalize(const int* cnt, const int* list, const double* list_score, int N, int H, int W,
                            const RecordLayout& L, uint8_t* records, int* peak_pos, int* part_cnt, hipStream_t st);
 void launch_paf_score(const PafScales& S, const int* peak_pos, const int* part_cnt, int N, int cap, double thre2,
@@ -102,7 +103,9 @@ void launch_assemble(const Conn* conn, const int* conn_cnt, const int* part_cnt,
 
 // hand.hip
 size_t hand_cc_workspace_bytes(int NP);
+// tile_seeds: lab labelled per gauss_threshold tile (only tile edges left to join); else run seeds
+// (blur5_seed)
 void launch_hand_cc(double* avg, int NP, int H, int W, int* lab, double* sums, const int* cnt, double* peaks,
-                    int* found, void* ws, hipStream_t st);
+                    int* found, void* ws, bool tile_seeds, hipStream_t st);
 
 }  // namespace opose

@@ -381,8 +381,9 @@ void launch_gauss_nms_resize(const float* mid, int Cm, int coff, int P, int N, i
                        cap, cnt, list, list_score);
 }
 
-// Hand: binary = gaussian_filter(map) > thre (src/hand.py:62-63) as union-find seeds:
-// lab[i] = start of i's run within its 64-pixel segment where set, -1 elsewhere; cnt[np] += #set.
+// Hand: binary = gaussian_filter(map) > thre (src/hand.py:62-63) as union-find seeds, labelled
+// within each 64 x 32 tile: lab[i] = the first pixel (raster order) of i's component inside
+// the tile where set, -1 elsewhere; cnt[np] += #set.
 __global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict__ avg, int H, int W, double thre,
                                                        int* __restrict__ lab, int* __restrict__ cnt) {
     __shared__ GaussTile t;
@@ -399,24 +400,79 @@ __global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict_
         return;
     }
     int mine = 0;
-    // a wave = one 64-pixel row segment of the tile: each set pixel points at the start of its
-    // run inside the segment (union-find parent < itself), so cc_union only links runs
+    // The tile's own 8-connected components, in LDS (the vertical-pass plane is free now): a
+    // wave = one 64-pixel tile row; each set pixel starts at the first pixel of its run (parent
+    // < itself), runs are linked to the runs above them (one union per run contact, as in
+    // cc_union), then every pixel stores the global index of its local root -- the component's
+    // first pixel in raster order within the tile.  cc_border joins components across tiles.
+    static_assert(TW == 64 && sizeof(t.v) >= sizeof(int) * TW * TH, "tile labels");
+    int* sl = reinterpret_cast<int*>(&t.v[0][0]);
     const int lane = threadIdx.x & 63;
     for (int e = threadIdx.x; e < TW * TH; e += 256) {
         const int r = e / TW, c = e - r * TW;
-        const int y = y0 + r, x = x0 + c;
-        const bool in = y < H && x < W;
-        const bool on = in && t.g[r + 1][c + 1] > thre;
+        const bool on = y0 + r < H && x0 + c < W && t.g[r + 1][c + 1] > thre;
         const unsigned long long unset = ~__ballot(on) & ((1ull << lane) - 1);  // unset lanes below
         const int start = unset ? 64 - __clzll((long long)unset) : 0;          // first lane of the run
-        if (!in) continue;
-        const int i = y * W + x;
-        lab[(size_t)np * H * W + i] = on ? i - (lane - start) : -1;
+        sl[e] = on ? e - (lane - start) : -1;
         mine += on;
+    }
+    __syncthreads();
+    const volatile int* vsl = sl;  // re-read: other lanes relink roots concurrently
+    auto find = [&](int x) __attribute__((always_inline)) {
+        int p = vsl[x];
+        while (p != x) {
+            x = p;
+            p = vsl[x];
+        }
+        return x;
+    };
+    auto unite = [&](int a, int b) __attribute__((always_inline)) {
+        for (;;) {
+            a = find(a);
+            b = find(b);
+            if (a == b) return;
+            if (a < b) {
+                const int tmp = a;
+                a = b;
+                b = tmp;
+            }
+            const int old = atomicMin(sl + a, b);  // link root a (larger) under b
+            if (old == a) return;
+            a = old;
+        }
+    };
+    for (int e = threadIdx.x + TW; e < TW * TH; e += 256) {
+        if (sl[e] < 0) continue;
+        const int c = e & (TW - 1), u = e - TW;
+        const bool left = c > 0 && sl[e - 1] >= 0;
+        const bool ul = c > 0 && sl[u - 1] >= 0, up = sl[u] >= 0, ur = c + 1 < TW && sl[u + 1] >= 0;
+        if (!left) {
+            if (ul) unite(e, u - 1);
+            if (up && !ul) unite(e, u);
+        }
+        if (ur && !up) unite(e, u + 1);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < TW * TH; e += 256) {
+        const int r = e / TW, c = e - r * TW;
+        const int y = y0 + r, x = x0 + c;
+        if (y >= H || x >= W) continue;
+        int g = -1;
+        if (sl[e] >= 0) {
+            const int root = find(e);
+            g = (y0 + root / TW) * W + x0 + (root & (TW - 1));
+        }
+        lab[(size_t)np * H * W + y * W + x] = g;
     }
     if (mine) atomicAdd(&s_n, mine);
     __syncthreads();
     if (threadIdx.x == 0 && s_n) atomicAdd(cnt + np, s_n);
+}
+
+// tiles of gauss_threshold (per map); cc_border's grid
+void gauss_threshold_tiles(int H, int W, int* ntx, int* nty) {
+    *ntx = (W + TW - 1) / TW;
+    *nty = (H + TH - 1) / TH;
 }
 
 // ---------------------------------------------------------------- Batch_body fast mode

@@ -63,16 +63,16 @@ def test_hand_batch_and_all_missing(hand):
     assert z.dtype == np.int64 and not z.any()
 
 
-@pytest.mark.parametrize("seed", [0, 1, 2, 3])
-def test_hand_post_intricate_components(hand, seed):
+@pytest.mark.parametrize("seed,S", [(0, 120), (1, 120), (2, 120), (3, 120), (4, 368), (5, 368)])
+def test_hand_post_intricate_components(hand, seed, S):
     """Heat maps hovering around the threshold: many components with holes, diagonal-only
-    contacts and long snakes after the x8 upsample + Gaussian -- the labelling, the sums and
-    the selection must match the oracle (scipy.ndimage.label) exactly."""
+    contacts and long snakes after the x8 upsample + Gaussian -- the labelling (per 64 x 32
+    tile in LDS, then joined across tile edges: 2 x 4 tiles at S = 120, 6 x 12 at 368), the
+    sums and the selection must match the oracle (scipy.ndimage.label) exactly."""
     from scipy.ndimage import gaussian_filter
     from oracle import hand_post
     from oracle.body_post import preprocess
     rng = np.random.default_rng(100 + seed)
-    S = 120
     maps, lowres, pads = [], [], []
     for s in SCALES:
         _, pad, padded_hw = preprocess(np.zeros((S, S, 3), np.uint8), s * 368 / S)
