@@ -320,18 +320,16 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     // ---- epilogue: a piece of a shared tile leaves an fp32 partial slab (summed in k order by
     // conv_x6_fixup); a whole tile adds bias + ReLU and writes X6 / X6P slices or fp32 NCHW
     if (c_begin != 0 || c_end != nK) {
-        float* slab = a.partial + (size_t)(2 * id + (first ? 0 : 1)) * (MT * PT);
+        const __amdgpu_buffer_rsrc_t srs = slab_rsrc(a.partial);
+        const uint32_t sbase = (uint32_t)(2 * id + (first ? 0 : 1)) * (uint32_t)(MT * PT * 4);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int pl = wp0 + j * 16 + (lane & 15);
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int ml = wm0 + i * 16 + 4 * (lane >> 4) + t;
-                    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(slab + ml * PT + pl), "v"(acc[i][j][t])
-                                 : "memory");
-                }
+            for (int i = 0; i < TM; ++i) {
+                const int q = (wm0 + i * 16) / 4 + (lane >> 4);
+                store_slab_quad(srs, sbase + (uint32_t)(q * PT + pl) * 16u, acc[i][j]);
+            }
         }
         continue;
     }

@@ -357,7 +357,6 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         // column (pixel) pl.  32x32: quad qd covers rows 32i + 8qd + 4hk .. +3, pixel 32j + l31;
         // 16x16: rows 16i + 4(l >> 4) .. +3, pixel 16j + (l & 15).
         const bool whole = c_begin == 0 && c_end == nK;
-        float* slab = a.partial + (size_t)(2 * id + (first ? 0 : 1)) * (MT * PT);
         const int cout8 = (G.cout + 7) & ~7;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -368,15 +367,12 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
                 return wm0 + i * 16 + 4 * (lane >> 4);
             };
             if (!whole) {
+                static_assert(ACC_N == 4, "slab quads: one 16x16 accumulator block per lane quad");
+                const __amdgpu_buffer_rsrc_t srs = slab_rsrc(a.partial);
+                const uint32_t sbase = (uint32_t)(2 * id + (first ? 0 : 1)) * (uint32_t)(MT * PT * 4);
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int r = 0; r < ACC_N; ++r) {
-                        const int ml = quad_row(i, r >> 2) + (r & 3);
-                        asm volatile("global_store_dword %0, %1, off sc1" ::"v"(slab + ml * PT + pl),
-                                     "v"(acc[i][j][r])
-                                     : "memory");
-                    }
+                    store_slab_quad(srs, sbase + (uint32_t)((quad_row(i, 0) / 4) * PT + pl) * 16u, acc[i][j]);
                 continue;
             }
             if (a.pool) {
@@ -467,8 +463,8 @@ __device__ __forceinline__ void store8_x6(uint8_t* unit, uint32_t ps, const floa
 
 // Stream-K fixup: grid (tiles, MT*PT/8/256); each thread finishes one X6 unit (8 channels of one
 // pixel) of a shared tile: partial slabs summed in k order (deterministic).  Pixels run fastest
-// across the lanes, so every slab load is a coalesced 256-byte row segment and every store a
-// whole 16-byte unit; two slabs' loads are in flight per round trip.
+// across the lanes, so every slab load is a coalesced 1 KB run of channel quads (x6.h) and every
+// store a whole 16-byte unit; two slabs' loads are in flight per round trip.
 template <int MT, int PT>
 __global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
     const int nM = a.Mpad / MT;
@@ -491,33 +487,40 @@ __global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
     if (p >= G.npix) return;
     const int cout8 = (G.cout + 7) & ~7;
     if (mg >= (G.out_f32 ? G.cout : cout8)) return;
+    // the unit's two channel quads (x6.h slab layout): quads ml0/4 and ml0/4 + 1 of pixel pl
     auto slab = [&](int w) __attribute__((always_inline)) {
         const long long lo_w = (long long)w * I / Gw;
         const int slot = (lo_w / nK == tile) ? 2 * w : 2 * w + 1;
-        return a.partial + (size_t)slot * (MT * PT) + (size_t)ml0 * PT + pl;
+        return reinterpret_cast<const f32x4*>(a.partial + (size_t)slot * (MT * PT)) + (size_t)(ml0 / 4) * PT + pl;
     };
     float v[8];
     {
-        const float* s = slab(w0);
+        const f32x4* s = slab(w0);
+        const f32x4 lo = s[0], hi = s[PT];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = s[(size_t)t * PT];
+        for (int t = 0; t < 4; ++t) {
+            v[t] = lo[t];
+            v[4 + t] = hi[t];
+        }
     }
     int w = w0 + 1;
     for (; w < w1; w += 2) {
-        const float *s0 = slab(w), *s1 = slab(w + 1);
-        float x0v[8], x1v[8];
+        const f32x4 *s0 = slab(w), *s1 = slab(w + 1);
+        const f32x4 a0 = s0[0], a1 = s0[PT], b0 = s1[0], b1 = s1[PT];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            x0v[t] = s0[(size_t)t * PT];
-            x1v[t] = s1[(size_t)t * PT];
+        for (int t = 0; t < 4; ++t) {
+            v[t] = (v[t] + a0[t]) + b0[t];
+            v[4 + t] = (v[4 + t] + a1[t]) + b1[t];
         }
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = (v[t] + x0v[t]) + x1v[t];
     }
     if (w == w1) {
-        const float* s = slab(w);
+        const f32x4* s = slab(w);
+        const f32x4 lo = s[0], hi = s[PT];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] += s[(size_t)t * PT];
+        for (int t = 0; t < 4; ++t) {
+            v[t] += lo[t];
+            v[4 + t] += hi[t];
+        }
     }
 #pragma unroll
     for (int t = 0; t < 8; ++t) {

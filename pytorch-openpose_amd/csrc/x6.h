@@ -48,6 +48,19 @@ __device__ __forceinline__ void store4_x6(uint8_t* unit, uint32_t ps, const floa
     }
 }
 
+// Stream-K partial slabs (X6Args::partial): per workgroup piece an fp32 [MT/4][PT] array of
+// channel quads -- quad q (channels 4q .. 4q+3 of the tile), pixel pl at float index
+// (q * PT + pl) * 4.  A lane's accumulator block holds 4 consecutive channels of one pixel, so
+// it leaves the kernel as one 16-byte write-through (sc1) store; conv_x6_fixup reads two quads
+// per X6 unit.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(float* partial) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)partial, (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void store_slab_quad(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, f32x4 v) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)byte_off, 0, 16);  // aux 16: sc1
+}
+
 // unit index of (frame n, group g of the slice, y, x) in an X6 plane (common.h X6Layout)
 __device__ __forceinline__ uint32_t x6_unit(const X6Layout& l, int n, int g, int y, int x) {
     return l.o0 + (uint32_t)n * l.fs + (uint32_t)g * l.gs + (uint32_t)y * l.rs + (uint32_t)x;
