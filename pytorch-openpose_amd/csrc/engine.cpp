@@ -972,6 +972,8 @@ struct NetSeg {
     int slot;  // workspace set (opose_ctx::ws)
 };
 
+static void run_scales_concurrently(opose_ctx* h, int ns, const std::function<void(int)>& fn);
+
 // VGG trunk on X6 activations: every segment's x -> its final trunk conv written via last[i]
 // (+ dup[i]).  Full and half resolution run on dense X6 buffers (A / B); from the second pool on
 // (H/4: conv3_x, H/8: conv4_x, conv5_x of the hand) the activations are padded X6P (P0 / P1,
@@ -1028,23 +1030,58 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
         uint8_t* p = lvl == 2 ? (avoid == b.P0 ? b.P1 : b.P0) : (avoid == b.Q0 ? b.Q1 : b.Q0);
         return x6pact(p, og, 0, N, hh, ww);
     };
+    // conv1_1 straight from the fp32 input (conv_first_x6, no input split) of segment i
+    auto conv11_direct = [&](size_t i, const Spec& s, DevConv* c) {
+        const NetSeg& sg = segs[i];
+        const size_t npix = (size_t)sg.N * sg.Hp * sg.Wp;
+        ProfEntry pe;
+        h->prof_begin(pe, "conv3x3", 2.0 * 64 * 27 * (double)npix, 0);
+        if (h->detail) pe.detail = "layer/" + s.name + "/first_direct/n" + std::to_string(npix);
+        launch_conv_first_x6(sg.x, sg.N, 3, sg.Hp, sg.Wp, c->wt, c->Mpad, c->bias, bs[i].A, (uint32_t)(npix * 8 * 16),
+                             h->stream);
+        h->prof_end(pe);
+        bs[i].cur = x6act(bs[i].A, 8, 0, sg.N, sg.Hp, sg.Wp);
+    };
+    // conv1_2 + pool with the input window in LDS instead of the 9-tap im2col stream (segment i,
+    // input at resolution level lvl)
+    auto conv12_win_ok = [&](const Spec& s, const DevConv* c) {
+        return h->fused_pool && h->win12 && s.name == "conv1_2" && c->cin == 64 && c->cout == 64 && c->ks == 3 &&
+               c->pad == 1 && c->Mpad == 64 && c->nK6 == 18 && !c->small6;
+    };
+    auto conv12_win = [&](size_t i, const Spec& s, DevConv* c, int lvl) {
+        const NetSeg& sg = segs[i];
+        const int og = (s.cout + 7) / 8;
+        const int hh = sg.Hp >> lvl, ww = sg.Wp >> lvl;
+        if (bs[i].cur.padded || bs[i].cur.l.fs != 8u * hh * ww) throw std::logic_error("conv1_2 input layout");
+        const size_t np = (size_t)sg.N * hh * ww, npo = (size_t)sg.N * (hh / 2) * (ww / 2);
+        const XAct out = out_buf(i, lvl + 1, og);
+        ProfEntry pe;
+        h->prof_begin(pe, "conv3x3", 2.0 * 64 * 576 * (double)(npo * 4), 0);
+        if (h->detail) pe.detail = "layer/" + s.name + "/x6win/n" + std::to_string(npo * 4);
+        launch_conv3_pool_win_x6(static_cast<const uint8_t*>(bs[i].cur.p), (uint32_t)(np * 8 * 16), sg.N, hh, ww,
+                                 c->wx6, c->bias, static_cast<uint8_t*>(out.p), (uint32_t)(npo * 8 * 16), h->stream);
+        h->prof_end(pe);
+        bs[i].cur = out;
+    };
     int lvl = 0;
     for (size_t li = 0; li < vgg.size(); ++li) {
         const Spec& s = vgg[li];
         DevConv* c = find_conv(h, net, s.name);
         if (li == 0 && s.cin == 3 && s.cout == 64 && s.ks == 3 && s.pad == 1 && vgg.size() > 1 && h->first_direct) {
-            // conv1_1 straight from the fp32 input (conv_first_x6), no input split
-            for (size_t i = 0; i < ns; ++i) {
-                const NetSeg& sg = segs[i];
-                const size_t npix = (size_t)sg.N * sg.Hp * sg.Wp;
-                ProfEntry pe;
-                h->prof_begin(pe, "conv3x3", 2.0 * 64 * 27 * (double)npix, 0);
-                if (h->detail) pe.detail = "layer/" + s.name + "/first_direct/n" + std::to_string(npix);
-                launch_conv_first_x6(sg.x, sg.N, 3, sg.Hp, sg.Wp, c->wt, c->Mpad, c->bias, bs[i].A,
-                                     (uint32_t)(npix * 8 * 16), h->stream);
-                h->prof_end(pe);
-                bs[i].cur = x6act(bs[i].A, 8, 0, sg.N, sg.Hp, sg.Wp);
+            DevConv* c2 = find_conv(h, net, vgg[1].name);
+            if (ns > 1 && ns <= (size_t)kMaxScales && h->scale_streams && conv12_win_ok(vgg[1], c2)) {
+                // a pyramid's conv1_1 -> conv1_2 chains (their own kernels, one launch per
+                // segment) on concurrent streams: the small scales' launches fill the large
+                // scale's tail instead of running one after another
+                run_scales_concurrently(h, (int)ns, [&](int i) {
+                    conv11_direct((size_t)i, s, c);
+                    conv12_win((size_t)i, vgg[1], c2, 0);
+                });
+                ++li;
+                ++lvl;
+                continue;
             }
+            for (size_t i = 0; i < ns; ++i) conv11_direct(i, s, c);
             continue;
         }
         if (li == 0) {
@@ -1062,24 +1099,8 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
         const bool final_layer = li + 1 == vgg.size();
         const int og = (s.cout + 7) / 8;
         const bool pooled = s.name == "conv1_2" || s.name == "conv2_2" || s.name == "conv3_4";
-        if (pooled && h->fused_pool && h->win12 && s.name == "conv1_2" && c->cin == 64 && c->cout == 64 && c->ks == 3 &&
-            c->pad == 1 && c->Mpad == 64 && c->nK6 == 18 && !c->small6) {
-            // conv1_2 + pool with the input window in LDS instead of the 9-tap im2col stream
-            for (size_t i = 0; i < ns; ++i) {
-                const NetSeg& sg = segs[i];
-                const int hh = sg.Hp >> lvl, ww = sg.Wp >> lvl;
-                if (bs[i].cur.padded || bs[i].cur.l.fs != 8u * hh * ww) throw std::logic_error("conv1_2 input layout");
-                const size_t np = (size_t)sg.N * hh * ww, npo = (size_t)sg.N * (hh / 2) * (ww / 2);
-                const XAct out = out_buf(i, lvl + 1, og);
-                ProfEntry pe;
-                h->prof_begin(pe, "conv3x3", 2.0 * 64 * 576 * (double)(npo * 4), 0);
-                if (h->detail) pe.detail = "layer/" + s.name + "/x6win/n" + std::to_string(npo * 4);
-                launch_conv3_pool_win_x6(static_cast<const uint8_t*>(bs[i].cur.p), (uint32_t)(np * 8 * 16), sg.N, hh,
-                                         ww, c->wx6, c->bias, static_cast<uint8_t*>(out.p), (uint32_t)(npo * 8 * 16),
-                                         h->stream);
-                h->prof_end(pe);
-                bs[i].cur = out;
-            }
+        if (pooled && conv12_win_ok(s, c)) {
+            for (size_t i = 0; i < ns; ++i) conv12_win(i, s, c, lvl);
             ++lvl;
             continue;
         }
