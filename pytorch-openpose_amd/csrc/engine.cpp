@@ -126,6 +126,30 @@ struct DevBuf {
     }
 };
 
+// Pinned host staging (small results copied back each call: a device-to-host copy into pageable
+// memory goes through the runtime's staging buffer, ~35 us per copy on the box)
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    template <class T>
+    T* ensure(size_t n) {
+        const size_t b = n * sizeof(T);
+        if (b > bytes) {
+            if (p) {
+                OPOSE_HIP_CHECK(hipDeviceSynchronize());  // a copy into it may still be in flight
+                OPOSE_HIP_CHECK(hipHostFree(p));
+                p = nullptr;
+            }
+            OPOSE_HIP_CHECK(hipHostMalloc(&p, b, hipHostMallocDefault));
+            bytes = b;
+        }
+        return static_cast<T*>(p);
+    }
+};
+
 // A GEMM-ready conv: one or two (combined) reference layers.
 struct DevConv {
     std::string name;
@@ -235,6 +259,7 @@ struct opose_ctx {
     }();
     DevBuf frames, mids[2][kMaxScales], avg, cnt, list, peak_pos, part_cnt, score, conn, conn_cnt, records, maps_in,
         hlab, hsums, hpeaks, hfound, list_score, hsel;
+    PinnedBuf hand_out;  // Hand() peaks + found, staged for the host
     // network workspace, one set per concurrently running scale (slot s runs on scale_stream(s);
     // slot 0 is the handle's stream): input, activations, stream-K slabs
     struct NetWS {
@@ -2300,7 +2325,7 @@ static void hand_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
               (size_t)out_crop * 21;
     OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * NP, h->stream));
     h->prof_begin(pe, "gauss_threshold", 0, (double)NP * H * W * 12);
-    launch_gauss_threshold(avg, NP, H, W, p.thre_hand, lab, cnt, h->stream);
+    launch_gauss_threshold(avg, NP, H, W, p.thre_hand, lab, cnt, sums, h->stream);
     h->prof_end(pe);
     h->prof_begin(pe, "hand_cc", 0, 0);
     void* ws = h->hsel.ensure<uint8_t>(hand_cc_workspace_bytes(NP), h->stream);
@@ -2312,11 +2337,15 @@ static void hand_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
 static void hand_finish(opose_ctx* h, int N, double* peaks_out, int32_t* found_out, int flags) {
     const int NP = N * 21;
     if (!(flags & OPOSE_OUT_DEVICE)) {
-        OPOSE_HIP_CHECK(hipMemcpyAsync(peaks_out, h->hpeaks.ensure<double>((size_t)NP * 3, h->stream),
-                                       sizeof(double) * NP * 3, hipMemcpyDeviceToHost, h->stream));
-        OPOSE_HIP_CHECK(hipMemcpyAsync(found_out, h->hfound.ensure<int>((size_t)NP, h->stream), sizeof(int) * NP,
+        double* st = h->hand_out.ensure<double>((size_t)NP * 4);  // NP * 3 peaks, then NP found
+        int32_t* sf = reinterpret_cast<int32_t*>(st + (size_t)NP * 3);
+        OPOSE_HIP_CHECK(hipMemcpyAsync(st, h->hpeaks.ensure<double>((size_t)NP * 3, h->stream), sizeof(double) * NP * 3,
+                                       hipMemcpyDeviceToHost, h->stream));
+        OPOSE_HIP_CHECK(hipMemcpyAsync(sf, h->hfound.ensure<int>((size_t)NP, h->stream), sizeof(int) * NP,
                                        hipMemcpyDeviceToHost, h->stream));
         OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+        std::memcpy(peaks_out, st, sizeof(double) * NP * 3);
+        std::memcpy(found_out, sf, sizeof(int32_t) * NP);
     }
     h->prof_drain();
 }

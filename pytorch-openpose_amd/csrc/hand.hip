@@ -234,7 +234,8 @@ void launch_hand_cc(double* avg, int NP, int H, int W, int* lab, double* sums, c
     } else {
         hipLaunchKernelGGL(cc_union, grid, dim3(256), 0, st, lab, H, W);
     }
-    OPOSE_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(double) * (size_t)NP * H * W, st));
+    if (!tile_seeds)  // tile seeds: gauss_threshold zeroed the sums at every possible root
+        OPOSE_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(double) * (size_t)NP * H * W, st));
     hipLaunchKernelGGL(cc_compress_sum, grid, dim3(256), 0, st, lab, avg, H, W, sums);
     double* part_v = static_cast<double*>(ws);
     int* part_i = reinterpret_cast<int*>(part_v + (size_t)NP * SEL_NB);

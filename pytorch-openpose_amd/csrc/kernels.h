@@ -90,7 +90,9 @@ void launch_blur5_nms(const float* heat, int NP, int H, int W, double thre, int 
 // Batch_hand fast mode: blurred (5x5, float64 out) + union-find seeds of blurred > thre
 void launch_blur5_seed(const float* heat, int NP, int H, int W, double thre, double* blurred, int* lab, int* cnt,
                        hipStream_t st);
-void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st);
+// sums: zeroed at every tile-local root (the component sums' only addresses; launch_hand_cc)
+void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, double* sums,
+                            hipStream_t st);
 void gauss_threshold_tiles(int H, int W, int* ntx, int* nty);
 void launch_peaks_finalize(const int* cnt, const int* list, const double* list_score, int N, int H, int W,
                            const RecordLayout& L, uint8_t* records, int* peak_pos, int* part_cnt, hipStream_t st);

@@ -385,7 +385,8 @@ void launch_gauss_nms_resize(const float* mid, int Cm, int coff, int P, int N, i
 // within each 64 x 32 tile: lab[i] = the first pixel (raster order) of i's component inside
 // the tile where set, -1 elsewhere; cnt[np] += #set.
 __global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict__ avg, int H, int W, double thre,
-                                                       int* __restrict__ lab, int* __restrict__ cnt) {
+                                                       int* __restrict__ lab, int* __restrict__ cnt,
+                                                       double* __restrict__ sums) {
     __shared__ GaussTile t;
     __shared__ int s_n;
     int x0, y0, np;
@@ -461,6 +462,9 @@ __global__ __launch_bounds__(256) void gauss_threshold(const double* __restrict_
         if (sl[e] >= 0) {
             const int root = find(e);
             g = (y0 + root / TW) * W + x0 + (root & (TW - 1));
+            // every component's root is one of its tiles' local roots: the sums cc_compress_sum
+            // accumulates start from these zeros (no memset of the whole map)
+            if (root == e) sums[(size_t)np * H * W + g] = 0.0;
         }
         lab[(size_t)np * H * W + y * W + x] = g;
     }
@@ -973,9 +977,10 @@ void launch_blur5_seed(const float* heat, int NP, int H, int W, double thre, dou
     hipLaunchKernelGGL(blur5_seed, grid, dim3(256), 0, st, heat, H, W, thre, blurred, lab, cnt);
 }
 
-void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, hipStream_t st) {
+void launch_gauss_threshold(const double* avg, int NP, int H, int W, double thre, int* lab, int* cnt, double* sums,
+                            hipStream_t st) {
     dim3 grid(((W + TW - 1) / TW) * ((H + TH - 1) / TH) * NP);
-    hipLaunchKernelGGL(gauss_threshold, grid, dim3(256), 0, st, avg, H, W, thre, lab, cnt);
+    hipLaunchKernelGGL(gauss_threshold, grid, dim3(256), 0, st, avg, H, W, thre, lab, cnt, sums);
 }
 
 void launch_peaks_finalize(const int* cnt, const int* list, const double* list_score, int N, int H, int W,
