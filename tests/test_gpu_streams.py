@@ -97,8 +97,9 @@ def test_pipelined_multiscale_matches_serial():
 
 
 def test_hand_scale_streams_bit_identical():
-    """Hand(): the four scales on concurrent streams (default) and one after another
-    (OPOSE_SCALE_STREAMS=0, read when the handle is created) give identical peaks."""
+    """Hand(): the per-scale work that runs on concurrent streams by default (the lockstep
+    pyramid's conv1_1 -> conv1_2 chains, one stream per scale) and the same work one launch
+    after another (OPOSE_SCALE_STREAMS=0, read when the handle is created) give identical peaks."""
     from src.hand import Hand
     from src.weights import seeded_state_dict
     crop = np.random.default_rng(14).integers(0, 256, (150, 150, 3), dtype=np.uint8)
