@@ -319,21 +319,10 @@ __global__ __launch_bounds__(256) void gauss_nms_resize(const float* __restrict_
         // nothing to resize, filter or report (the exact criterion gauss_wide_tail applies to
         // the resized values, taken earlier and more conservatively).  NaN sources count as
         // below, as in gauss_wide_tail (a NaN only ever removes peaks).
+        // One pass over the source: the horizontal resize of every footprint row goes to LDS
+        // while the same loads feed the bound (a cold tile then returns without a second read
+        // of its sources; a hot one has its rows staged already)
         float mx = 0.f;
-        for (int r0 = lo + h; r0 <= hi; r0 += 16) {
-            float q[8][4];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const float* row = plane + (size_t)min(r0 + 2 * k, hi) * Ws;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) q[k][j] = row[tx.i[j]];
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) mx = fmaxf(mx, fabsf(q[k][j]));
-        }
-        if (!__syncthreads_or(1.9 * (double)mx >= gauss_skip_below(thre))) return;
         for (int r0 = lo + h; r0 <= hi; r0 += 16) {  // 8 rows per round, loads issued first
             float q[8][4];
 #pragma unroll
@@ -344,6 +333,8 @@ __global__ __launch_bounds__(256) void gauss_nms_resize(const float* __restrict_
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) mx = fmaxf(mx, fabsf(q[k][j]));
                 float v = q[k][0] * tx.c[0];
                 v = v + q[k][1] * tx.c[1];
                 v = v + q[k][2] * tx.c[2];
@@ -351,8 +342,9 @@ __global__ __launch_bounds__(256) void gauss_nms_resize(const float* __restrict_
                 if (r0 + 2 * k <= hi) hs[r0 + 2 * k - lo][c] = v;
             }
         }
+        // (the vote is also the barrier before the vertical pass reads hs)
+        if (!__syncthreads_or(1.9 * (double)mx >= gauss_skip_below(thre))) return;
     }
-    __syncthreads();
     double win[WVH + 24];
 #pragma unroll
     for (int i = 0; i < WVH + 24; ++i) {
