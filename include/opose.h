@@ -243,6 +243,13 @@ int opose_debug_preprocess(opose_t* h, const uint8_t* bgr, int H, int W, double 
  * (optional) the x8-upsampled, cropped PAF maps [38,Hs,Ws] float32 */
 int opose_debug_heat(opose_t* h, const float* maps, int hl, int wl, int pad_down, int pad_right, int H, int W,
                      double* heat_avg, float* paf_mid);
+/* src/hand.py:62-64 on NP float64 maps [NP,H,W]: binary = gaussian_filter(map, 3) > thre, then
+ * label(binary, connectivity 2) -> labels [NP,H,W] int32: -1 off the binary map, else the
+ * linear index (y * W + x) of the component's first pixel in raster order -- scipy.ndimage.label's
+ * numbering order -- and sums [NP,H,W] float64: at a component's first pixel, the sum of the
+ * map over the component (elsewhere undefined) */
+int opose_debug_hand_label(opose_t* h, const double* maps, int NP, int H, int W, double thre, int32_t* labels,
+                           double* sums);
 
 #ifdef __cplusplus
 }

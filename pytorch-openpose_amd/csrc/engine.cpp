@@ -2839,6 +2839,30 @@ int opose_debug_heat(opose_t* h, const float* maps, int hl, int wl, int pad_down
     return OPOSE_OK;
 }
 
+int opose_debug_hand_label(opose_t* h, const double* maps, int NP, int H, int W, double thre, int32_t* labels,
+                           double* sums) {
+    if (!h || !maps || !labels || !sums || NP <= 0 || H <= 0 || W <= 0) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        enter_main(h);
+        const size_t n = (size_t)NP * H * W;
+        DevBuf mb, lb, sb, cb, pk, fd, ws;
+        double* md = mb.ensure<double>(n, h->stream);
+        int* lab = lb.ensure<int>(n, h->stream);
+        double* sd = sb.ensure<double>(n, h->stream);
+        int* cnt = cb.ensure<int>((size_t)NP, h->stream);
+        OPOSE_HIP_CHECK(hipMemcpyAsync(md, maps, n * 8, hipMemcpyHostToDevice, h->stream));
+        OPOSE_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * NP, h->stream));
+        launch_gauss_threshold(md, NP, H, W, thre, lab, cnt, sd, h->stream);
+        launch_hand_cc(md, NP, H, W, lab, sd, cnt, pk.ensure<double>((size_t)NP * 3, h->stream),
+                       fd.ensure<int>((size_t)NP, h->stream), ws.ensure<uint8_t>(hand_cc_workspace_bytes(NP), h->stream),
+                       true, h->stream);
+        OPOSE_HIP_CHECK(hipMemcpyAsync(labels, lab, n * 4, hipMemcpyDeviceToHost, h->stream));
+        OPOSE_HIP_CHECK(hipMemcpyAsync(sums, sd, n * 8, hipMemcpyDeviceToHost, h->stream));
+        OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+    });
+    return OPOSE_OK;
+}
+
 int opose_profile_enable(opose_t* h, int enable) {
     if (!h) return OPOSE_E_ARG;
     h->prof = enable != 0;

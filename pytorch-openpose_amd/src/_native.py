@@ -69,6 +69,7 @@ def _load():
         "opose_debug_conv_x6": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P]),
         "opose_debug_conv_x6_time": (I, [P, I, I, I, I, I, I, I, I, I, I, I, P]),
         "opose_debug_heat": (I, [P, P, I, I, I, I, I, I, P, P]),
+        "opose_debug_hand_label": (I, [P, P, I, I, I, D, P, P]),
     }
     for name, (res, args) in sig.items():
         if "OPOSE_LIB" in os.environ and not hasattr(lib, name):
@@ -90,7 +91,7 @@ EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last
             "opose_body_post", "opose_body_scale_geom", "opose_body_scale_maps",
             "opose_body_post_scales", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
             "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_conv_time", "opose_debug_conv_x6", "opose_debug_conv_x6_time", "opose_debug_preprocess",
-            "opose_debug_heat"]
+            "opose_debug_heat", "opose_debug_hand_label"]
 
 
 class OposeError(RuntimeError):

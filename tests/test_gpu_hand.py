@@ -86,3 +86,40 @@ def test_hand_post_intricate_components(hand, seed, S):
     out = hand.post(maps, pads, S, S)[0]
     assert out.dtype == ref.dtype
     assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("shape", [(368, 368), (100, 70), (33, 200)])
+def test_hand_labels_match_scipy(hand, shape):
+    """The labelling itself (gauss_threshold's per-tile components in LDS + cc_border across tile
+    edges + cc_compress_sum), label for label: binary = gaussian_filter(map, 3) > thre and
+    scipy.ndimage.label(binary, 8-connectivity) (src/hand.py:62-64), each component named by its
+    first pixel in raster order (scipy's numbering order).  Maps hover around the threshold so
+    the components are many, holed, snaking and diagonal-only-connected; the shapes leave ragged
+    64 x 32 tiles at the right and bottom edges.  Component sums against numpy at 1e-12."""
+    from scipy.ndimage import gaussian_filter, label
+    from src import _native
+    H, W = shape
+    rng = np.random.default_rng(H * 7 + W)
+    NP = 3
+    noise = gaussian_filter(rng.standard_normal((NP, H, W)), (0, 2.5, 2.5))
+    maps = np.ascontiguousarray(0.05 + 0.1 * noise / noise.std())
+    thre = 0.05
+    labels = np.empty((NP, H, W), np.int32)
+    sums = np.empty((NP, H, W), np.float64)
+    hand.handle.check(_native.lib.opose_debug_hand_label(hand.handle.h, maps.ctypes.data, NP, H, W, thre,
+                                                         labels.ctypes.data, sums.ctypes.data))
+    ncomp = 0
+    for k in range(NP):
+        binary = gaussian_filter(maps[k], sigma=3) > thre
+        lab, n = label(binary, structure=np.ones((3, 3), int))
+        ncomp += n
+        flat = lab.ravel()
+        first = np.zeros(n + 1, np.int64)  # first (raster-order) pixel of each scipy label
+        idx = np.flatnonzero(flat)
+        first[1:] = np.full(n, flat.size)
+        np.minimum.at(first, flat[idx], idx)
+        expect = np.where(flat > 0, first[flat], -1).reshape(H, W)
+        assert np.array_equal(labels[k], expect.astype(np.int32)), k
+        ref_sums = np.bincount(flat, weights=maps[k].ravel(), minlength=n + 1)[1:]
+        np.testing.assert_allclose(sums[k].ravel()[first[1:]], ref_sums, rtol=1e-12, atol=1e-12)
+    assert ncomp > 10
