@@ -812,7 +812,9 @@ void launch_from_x6(const uint8_t* in, int cg, int goff, uint32_t ps, int C, int
 // implicit GEMM would pad K = 27 to 3 chunks of 32 and spend the launch on tile prologues; this
 // kernel is bound by its 384-byte-per-pixel X6 store.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-template <int CIN>
+// F32OUT: the 64 channels as fp32 units of 8 channels (32 bytes, [N][8][H*W] units) for
+// conv3_pool_win_x6<true>, which splits them itself: 256 instead of 384 bytes per pixel.
+template <int CIN, bool F32OUT>
 __global__ __launch_bounds__(256) void conv_first_x6_kernel(const float* __restrict__ x, int N, int H, int W,
                                                             const float* __restrict__ wt, int Mpad,
                                                             const float* __restrict__ bias, uint8_t* __restrict__ out,
@@ -862,6 +864,12 @@ __global__ __launch_bounds__(256) void conv_first_x6_kernel(const float* __restr
                 v[2 * q] = fmaxf(acc[q].x + s_b[g * 8 + 2 * q], 0.f);
                 v[2 * q + 1] = fmaxf(acc[q].y + s_b[g * 8 + 2 * q + 1], 0.f);
             }
+            if constexpr (F32OUT) {
+                float4* u = reinterpret_cast<float4*>(out + (((size_t)n * 8 + g) * HW + r) * 32);
+                u[0] = make_float4(v[0], v[1], v[2], v[3]);
+                u[1] = make_float4(v[4], v[5], v[6], v[7]);
+                continue;
+            }
             uint32_t hp[3][8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) split3(v[k], hp[0][k], hp[1][k], hp[2][k]);
@@ -879,10 +887,15 @@ __global__ __launch_bounds__(256) void conv_first_x6_kernel(const float* __restr
 }
 
 void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const float* wt, int Mpad, const float* bias,
-                          uint8_t* out, uint32_t ops, hipStream_t st) {
+                          uint8_t* out, uint32_t ops, bool f32_out, hipStream_t st) {
     if (Cin != 3) throw std::invalid_argument("conv_first_x6: Cin must be 3");
     const int grid = grid_for((size_t)N * H * W);
-    hipLaunchKernelGGL(conv_first_x6_kernel<3>, dim3(grid), dim3(256), 0, st, x, N, H, W, wt, Mpad, bias, out, ops);
+    if (f32_out)
+        hipLaunchKernelGGL((conv_first_x6_kernel<3, true>), dim3(grid), dim3(256), 0, st, x, N, H, W, wt, Mpad, bias,
+                           out, ops);
+    else
+        hipLaunchKernelGGL((conv_first_x6_kernel<3, false>), dim3(grid), dim3(256), 0, st, x, N, H, W, wt, Mpad, bias,
+                           out, ops);
 }
 
 // ---------------------------------------------------------------- windowed conv1_2 (+ pool)
@@ -923,6 +936,11 @@ struct WinSmem {
 };
 }  // namespace
 
+// F32IN: the input is conv_first_x6<.., true>'s fp32 units; each thread loads its window units
+// into registers and writes their three bf16 pieces (split3, as the X6 epilogue would have) into
+// the same LDS window (block 1's when every wave is past block 0's reads; the other workgroup on
+// the CU covers the load latency).
+template <bool F32IN>
 __global__ __launch_bounds__(256, 2) void conv3_pool_win_x6_kernel(const uint8_t* __restrict__ in, uint32_t ips,
                                                                    int N, int H, int W,
                                                                    const uint8_t* __restrict__ wt,
@@ -959,6 +977,61 @@ __global__ __launch_bounds__(256, 2) void conv3_pool_win_x6_kernel(const uint8_t
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sm.win + 64 * i), 16, off, 0, 0, 0);
         }
     };
+    // fp32 input: window slot u = tid + 256 k of block cb (k < 4, u < V_PP), 8 channels each, in
+    // named registers (an array here made the compiler put the fragment arrays in scratch, where
+    // the asm ds_reads' results were copied before they landed)
+    static_assert((V_PP + 255) / 256 == 4, "four window slots per thread");
+    f32x4 w0a, w0b, w1a, w1b, w2a, w2b, w3a, w3b;
+    auto load_slot = [&](int k, int cb, f32x4& a, f32x4& b) __attribute__((always_inline)) {
+        const int u = tid + 256 * k;
+        const int gl = u / V_GP, r = u - gl * V_GP;
+        const int wr = r / V_RP, wc = r - wr * V_RP;
+        const int iy = y0 - 1 + wr, ix = x0 - 1 + wc;
+        const bool ok = u < V_PP && wc < V_WC && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        // unconditional loads (a padding slot reads its frame's first pixel), then a select
+        const size_t off = ok ? ((size_t)(n * 8 + cb * 4 + gl) * HW + (size_t)iy * W + ix) * 32
+                              : (size_t)n * 8 * HW * 32;
+        const f32x4* src = reinterpret_cast<const f32x4*>(in + off);
+        const f32x4 a0 = src[0], a1 = src[1];
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        a = ok ? a0 : z;
+        b = ok ? a1 : z;
+    };
+    auto load_win32 = [&](int cb) __attribute__((always_inline)) {
+        load_slot(0, cb, w0a, w0b);
+        load_slot(1, cb, w1a, w1b);
+        load_slot(2, cb, w2a, w2b);
+        load_slot(3, cb, w3a, w3b);
+    };
+    auto store_slot = [&](int k, const f32x4& a, const f32x4& b) __attribute__((always_inline)) {
+        const int u = tid + 256 * k;
+        if (u >= V_PP) return;
+        uint32_t hp[3][8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            split3(a[e], hp[0][e], hp[1][e], hp[2][e]);
+            split3(b[e], hp[0][4 + e], hp[1][4 + e], hp[2][4 + e]);
+        }
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+            i32x4 w4;
+            w4[0] = (int)(hp[pc][0] | (hp[pc][1] << 16));
+            w4[1] = (int)(hp[pc][2] | (hp[pc][3] << 16));
+            w4[2] = (int)(hp[pc][4] | (hp[pc][5] << 16));
+            w4[3] = (int)(hp[pc][6] | (hp[pc][7] << 16));
+            // the window is only read by inline-asm ds_reads the compiler cannot see, so it is
+            // written by asm too (waited for with an explicit lgkmcnt before the barrier that
+            // publishes it)
+            const uint32_t wa = (uint32_t)(uintptr_t)(lds_ptr_t)(sm.win + pc * V_PP + u);
+            asm volatile("ds_write_b128 %0, %1\n\ts_nop 1" ::"v"(wa), "v"(w4) : "memory");
+        }
+    };
+    auto store_win32 = [&]() __attribute__((always_inline)) {
+        store_slot(0, w0a, w0b);
+        store_slot(1, w1a, w1b);
+        store_slot(2, w2a, w2b);
+        store_slot(3, w3a, w3b);
+    };
     auto dma_a = [&](int c, int st) __attribute__((always_inline)) {
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(wt + (size_t)c * 12 * 64 * 16), (short)0, (int)0x7fffffff, 0x00020000);
@@ -967,7 +1040,12 @@ __global__ __launch_bounds__(256, 2) void conv3_pool_win_x6_kernel(const uint8_t
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sm.a[st] + row * 64), 16,
                                                      (uint32_t)lane * 16u, row * 64 * 16, 0, 0);
     };
-    dma_win(0);
+    if constexpr (F32IN) {
+        load_win32(0);
+        store_win32();
+    } else {
+        dma_win(0);
+    }
     dma_a(0, 0);
     dma_a(1, 1);
     if (tid < 64) sm.b[tid] = bias[tid];
@@ -1027,39 +1105,51 @@ __global__ __launch_bounds__(256, 2) void conv3_pool_win_x6_kernel(const uint8_t
                         acc[nb][mb], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
     };
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // window block 0, weight chunks 0 and 1
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // window block 0, weight chunks 0 and 1
     __syncthreads();
     read_frags(0, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     fence_set(0);
     // chunk c's fragments are in register set c & 1 and its weights in stage c & 1; the reads of
     // chunk c + 1 are issued before chunk c's MFMAs and waited for after them
-#pragma unroll
-    for (int c = 0; c < 18; ++c) {
+    // (three loops, each fully unrolled: as one loop with chunk 8's window switch inside, the
+    // fp32-input instantiation was too large for the unroller, and a rolled loop keeps the
+    // fragment register sets in scratch)
+    auto chunk = [&](int c) __attribute__((always_inline)) {
         const int set = c & 1;
-        if (c == 8) {
-            // every wave is past chunk 7 (chunk 8's fragments in registers): block 1's window
-            // replaces block 0's and weight chunk 10 goes into chunk 8's stage, behind chunk 8's
-            // MFMAs
-            __syncthreads();
-            dma_win(1);
-            dma_a(10, 0);
-            mfma_chunk(set);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            read_frags(9, set ^ 1);
-        } else {
-            if (c + 1 < 18) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight chunk c + 1 (issued at c - 1)
-                __syncthreads();  // ... landed everywhere; every wave is past chunk c's reads
-                if (c + 2 < 18) dma_a(c + 2, c & 1);
-                read_frags(c + 1, set ^ 1);
-            }
-            mfma_chunk(set);
+        if (c + 1 < 18) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // weight chunk c + 1 (issued at c - 1)
+            __syncthreads();  // ... landed everywhere; every wave is past chunk c's reads
+            if (c + 2 < 18) dma_a(c + 2, c & 1);
+            read_frags(c + 1, set ^ 1);
         }
+        mfma_chunk(set);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         fence_set(set ^ 1);
+    };
+#pragma unroll
+    for (int c = 0; c < 8; ++c) chunk(c);
+    {
+        // every wave is past chunk 7 (chunk 8's fragments in registers): block 1's window
+        // replaces block 0's and weight chunk 10 goes into chunk 8's stage, behind chunk 8's
+        // MFMAs
+        __syncthreads();
+        if constexpr (F32IN) {
+            load_win32(1);
+            store_win32();
+        } else {
+            dma_win(1);
+        }
+        dma_a(10, 0);
+        mfma_chunk(0);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+        read_frags(9, 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        fence_set(1);
     }
+#pragma unroll
+    for (int c = 9; c < 18; ++c) chunk(c);
     // pooled epilogue: lane holds channels 16 mb + 4 gi + (0..3) of column q of block nb
     const int Wo = W >> 1, Ho = H >> 1;
     const size_t HWo = (size_t)Ho * Wo;
@@ -1087,12 +1177,16 @@ __global__ __launch_bounds__(256, 2) void conv3_pool_win_x6_kernel(const uint8_t
 }
 
 void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int W, const uint8_t* wt,
-                              const float* bias, uint8_t* out, uint32_t ops, hipStream_t st) {
+                              const float* bias, uint8_t* out, uint32_t ops, bool f32_in, hipStream_t st) {
     if (H < 2 || W < 2 || (size_t)N * 8 * H * W * 16 >= 0x80000000ull)
         throw std::invalid_argument("conv3_pool_win_x6: frame shape out of range");
     const int tiles = N * ((H + V_TH - 1) / V_TH) * ((W + V_TW - 1) / V_TW);
-    hipLaunchKernelGGL(conv3_pool_win_x6_kernel, dim3(tiles), dim3(64 * V_NW), 0, st, in, ips, N, H, W, wt, bias, out,
-                       ops);
+    if (f32_in)
+        hipLaunchKernelGGL(conv3_pool_win_x6_kernel<true>, dim3(tiles), dim3(64 * V_NW), 0, st, in, ips, N, H, W, wt,
+                           bias, out, ops);
+    else
+        hipLaunchKernelGGL(conv3_pool_win_x6_kernel<false>, dim3(tiles), dim3(64 * V_NW), 0, st, in, ips, N, H, W, wt,
+                           bias, out, ops);
 }
 
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,

@@ -245,6 +245,12 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_WIN_SK");
         return e && e[0] == '0';
     }();
+    // conv1_1 -> conv1_2 (window kernel) hand-off as fp32 units, split by conv1_2 (default);
+    // OPOSE_C11_F32=0: as X6 (A/B, bit-identical)
+    bool c11_f32 = [] {
+        const char* e = getenv("OPOSE_C11_F32");
+        return !(e && e[0] == '0');
+    }();
     // multi-frame segments whose windows overflow the LDS run as one segment per frame on the
     // window kernel (run_conv_x6_segs); OPOSE_SPLIT_FRAMES=0: conv_x6 for such launches (A/B)
     bool split_frames = [] {
@@ -1055,17 +1061,19 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
         uint8_t* p = lvl == 2 ? (avoid == b.P0 ? b.P1 : b.P0) : (avoid == b.Q0 ? b.Q1 : b.Q0);
         return x6pact(p, og, 0, N, hh, ww);
     };
-    // conv1_1 straight from the fp32 input (conv_first_x6, no input split) of segment i
-    auto conv11_direct = [&](size_t i, const Spec& s, DevConv* c) {
+    // conv1_1 straight from the fp32 input (conv_first_x6, no input split) of segment i; f32: its
+    // output as fp32 units for the windowed conv1_2, which splits them itself
+    auto conv11_direct = [&](size_t i, const Spec& s, DevConv* c, bool f32) {
         const NetSeg& sg = segs[i];
         const size_t npix = (size_t)sg.N * sg.Hp * sg.Wp;
         ProfEntry pe;
         h->prof_begin(pe, "conv3x3", 2.0 * 64 * 27 * (double)npix, 0);
         if (h->detail) pe.detail = "layer/" + s.name + "/first_direct/n" + std::to_string(npix);
         launch_conv_first_x6(sg.x, sg.N, 3, sg.Hp, sg.Wp, c->wt, c->Mpad, c->bias, bs[i].A, (uint32_t)(npix * 8 * 16),
-                             h->stream);
+                             f32, h->stream);
         h->prof_end(pe);
         bs[i].cur = x6act(bs[i].A, 8, 0, sg.N, sg.Hp, sg.Wp);
+        bs[i].cur.f32 = f32;  // (fp32 units at the X6 unit addresses x 2)
     };
     // conv1_2 + pool with the input window in LDS instead of the 9-tap im2col stream (segment i,
     // input at resolution level lvl)
@@ -1084,7 +1092,8 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
         h->prof_begin(pe, "conv3x3", 2.0 * 64 * 576 * (double)(npo * 4), 0);
         if (h->detail) pe.detail = "layer/" + s.name + "/x6win/n" + std::to_string(npo * 4);
         launch_conv3_pool_win_x6(static_cast<const uint8_t*>(bs[i].cur.p), (uint32_t)(np * 8 * 16), sg.N, hh, ww,
-                                 c->wx6, c->bias, static_cast<uint8_t*>(out.p), (uint32_t)(npo * 8 * 16), h->stream);
+                                 c->wx6, c->bias, static_cast<uint8_t*>(out.p), (uint32_t)(npo * 8 * 16),
+                                 bs[i].cur.f32, h->stream);
         h->prof_end(pe);
         bs[i].cur = out;
     };
@@ -1094,19 +1103,21 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
         DevConv* c = find_conv(h, net, s.name);
         if (li == 0 && s.cin == 3 && s.cout == 64 && s.ks == 3 && s.pad == 1 && vgg.size() > 1 && h->first_direct) {
             DevConv* c2 = find_conv(h, net, vgg[1].name);
-            if (ns > 1 && ns <= (size_t)kMaxScales && h->scale_streams && conv12_win_ok(vgg[1], c2)) {
+            const bool pair12 = conv12_win_ok(vgg[1], c2);
+            const bool f32 = pair12 && h->c11_f32;
+            if (ns > 1 && ns <= (size_t)kMaxScales && h->scale_streams && pair12) {
                 // a pyramid's conv1_1 -> conv1_2 chains (their own kernels, one launch per
                 // segment) on concurrent streams: the small scales' launches fill the large
                 // scale's tail instead of running one after another
                 run_scales_concurrently(h, (int)ns, [&](int i) {
-                    conv11_direct((size_t)i, s, c);
+                    conv11_direct((size_t)i, s, c, f32);
                     conv12_win((size_t)i, vgg[1], c2, 0);
                 });
                 ++li;
                 ++lvl;
                 continue;
             }
-            for (size_t i = 0; i < ns; ++i) conv11_direct(i, s, c);
+            for (size_t i = 0; i < ns; ++i) conv11_direct(i, s, c, f32);
             continue;
         }
         if (li == 0) {

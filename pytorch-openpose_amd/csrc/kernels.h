@@ -38,15 +38,17 @@ void launch_to_x6(const float* in, int cstride, int coff, int C, int N, int HW, 
                   uint32_t ps, hipStream_t st);
 void launch_from_x6(const uint8_t* in, int cg, int goff, uint32_t ps, int C, int N, int HW, float* out, int cstride,
                     int coff, hipStream_t st);
+// f32_out: fp32 units of 8 channels ([N][8][H*W] x 32 bytes) for launch_conv3_pool_win_x6's f32_in
 void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const float* wt, int Mpad, const float* bias,
-                          uint8_t* out, uint32_t ops, hipStream_t st);
+                          uint8_t* out, uint32_t ops, bool f32_out, hipStream_t st);
 // zero the padding units of `planes` X6P (piece, group) planes of an N x H x W buffer (common.h)
 void launch_x6p_clear_pads(uint8_t* const* bufs, const int* planes, int nbufs, int N, int H, int W, hipStream_t st);
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,
                        hipStream_t st);
-// conv1_2 (64 -> 64, 3x3 pad 1) + MaxPool2d(2, 2) from an 8-group X6 tensor, input window in LDS
+// conv1_2 (64 -> 64, 3x3 pad 1) + MaxPool2d(2, 2) from an 8-group X6 tensor (f32_in: fp32 units,
+// split in the kernel), input window in LDS
 void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int W, const uint8_t* wt,
-                              const float* bias, uint8_t* out, uint32_t ops, hipStream_t st);
+                              const float* bias, uint8_t* out, uint32_t ops, bool f32_in, hipStream_t st);
 // conv1x1_chain.hip: two chained 1x1 convs (CPM stage ends) in one launch, 64-pixel tiles
 void launch_conv1x1_chain_x6(const X6ChainArgs& a, hipStream_t st);
 // conv_win.hip: the 7x7 / 3x3 convs with the im2col operand from an LDS window of the padded X6P

@@ -189,6 +189,22 @@ def test_conv12_window_bit_identical(native, kind, shape):
         assert np.array_equal(a, r), kind
 
 
+@pytest.mark.parametrize("kind,shape", [("body", (2, 3, 72, 104)), ("body", (32, 3, 184, 328)),
+                                        ("hand", (1, 3, 88, 88))], ids=["body72x104", "bench32", "hand88"])
+def test_conv11_fp32_handoff_bit_identical(native, kind, shape):
+    """conv1_1 -> conv1_2 hand-off as fp32 units split inside conv3_pool_win_x6 (default) against
+    the X6 tensor split in conv1_1's epilogue (OPOSE_C11_F32=0): split3 of the same fp32 values
+    either way, so the network outputs are bit-identical (ragged 8 x 16 tiles at 72 x 104 / 88 x 88;
+    the bench's batch)."""
+    from src.model import bodypose_model, handpose_model
+    cls = bodypose_model if kind == "body" else handpose_model
+    x = np.random.default_rng(12).random(shape, dtype=np.float32) - np.float32(0.5)
+    on = _model_outputs(cls, kind, x, {"OPOSE_C11_F32": "1"})
+    off = _model_outputs(cls, kind, x, {"OPOSE_C11_F32": "0"})
+    for a, r in zip(on, off):
+        assert np.array_equal(a, r), kind
+
+
 @pytest.mark.parametrize("kind,shape", [("body", (32, 3, 184, 328)), ("body", (30, 3, 184, 328)),
                                         ("body", (88, 3, 136, 152)), ("hand", (120, 3, 184, 184))],
                          ids=["bench32", "partial_tile30", "frame_crossing88", "hand120"])
