@@ -60,6 +60,9 @@ enum {
                                 stream and overlaps the previous call's post-network
                                 part; records are still complete in the handle's stream
                                 order. Video-batch throughput mode.                 */
+    OPOSE_BAND_DP = 8,       /* opose_body_band_maps only: every banded conv on whole
+                                data-parallel tiles, so each output pixel sums in one
+                                fixed order whatever the band (bit-identical bands)  */
 };
 
 #define OPOSE_MAX_SCALES 8
@@ -152,6 +155,28 @@ int opose_body_scale_geom(int H, int W, const opose_params* p, int s, int* out4)
  * (channels 0..37 PAF, 38..56 heat), host memory unless OPOSE_OUT_DEVICE. */
 int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_t row_stride,
                           int64_t frame_stride, const opose_params* p, int s, float* maps, int flags);
+
+/* Row band [r0, r1) of scale s's network maps for ONE frame, for splitting a large scale across
+ * ranks (736x1312 is 53 % of the pyramid's FLOPs; src/body.py:36-50 for one
+ * m, cut into output rows).  Every rank of a band group runs the VGG trunk on the whole scale
+ * (30 % of the scale's FLOPs), then the six CPM stages (src/model.py:106-133) on its own rows
+ * only.  Before each 3x3 / 7x7 stage layer that needs them, the 3 rows on either side of the
+ * band are exchanged with the neighbouring bands: the library packs its top and bottom 3 rows
+ * into xbuf's send halves on its stream, calls fn(user, bytes, stream), and unpacks the recv
+ * halves.  fn moves send_up to the band above (its recv_dn) and send_dn to the band below (its
+ * recv_up), ordered on `stream` (a hipStream_t) or synchronously, and returns 0; it is called
+ * 27 times per frame and never for a single band covering every row.
+ *   xbuf: device memory, 4 x opose_body_band_halo_bytes(wl) bytes = [send_up | send_dn |
+ *         recv_up | recv_dn];  r1 - r0 >= 3;  maps [57, r1-r0, wl] fp32 (host unless
+ *         OPOSE_OUT_DEVICE);  bgr one H x W frame (device with OPOSE_IN_DEVICE);
+ *   OPOSE_BAND_DP: bit-identical banding (see the flag); default: stream-K grids per band.
+ * Concatenating every band's maps gives opose_body_scale_maps(s) within fp32 summation-order
+ * differences (split-bf16 accuracy). */
+typedef int (*opose_halo_fn)(void* user, size_t bytes, void* stream);
+size_t opose_body_band_halo_bytes(int wl);
+int opose_body_band_maps(opose_t* h, const uint8_t* bgr, int H, int W, int64_t row_stride,
+                         const opose_params* p, int s, int r0, int r1, float* maps,
+                         opose_halo_fn fn, void* user, void* xbuf, size_t xbuf_bytes, int flags);
 
 /* Multi-scale post-network body path (src/body.py:51-203): maps[s] = [N,57,hl[s],wl[s]] of
  * every scale (any rank's output of opose_body_scale_maps, gathered); the per-scale x8 /

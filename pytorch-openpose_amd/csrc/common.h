@@ -79,6 +79,8 @@ struct X6Group {
     int cout, relu, out_f32;
     int N, H, W;           // this group's frames (stride-1 'same' conv; pooled: the input's H, W)
     int npix;              // GEMM columns: N*H*W (pooled: N*(H/2)*(W/2)*4, quad-major)
+    int ylo, yhi;          // conv_x6 taps read rows [ylo, yhi) (yhi == 0: [0, H)); a row band's
+                           // view (engine.cpp Band) also reads its halo rows
     int t0;                // first tile of the group in the launch's tile space (set by the launcher)
 };
 

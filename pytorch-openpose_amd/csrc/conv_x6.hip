@@ -67,7 +67,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int nM = a.Mpad / MT;
     const int nK = a.nK;
     // geometry of the current tile's group (X6Group N, H, W, npix)
-    int H = 0, W = 0, HW = 0, npix = 0;
+    int H = 0, W = 0, HW = 0, npix = 0, ylo = 0, yspan = 0;
     // pooled conv (a.pool): GEMM columns run over the 2x2 quads of the pooled grid, quad-major
     // (column q -> pooled pixel q >> 2, quadrant q & 3), so the epilogue pools 4 adjacent lanes
     int Wo = 0, HWo = 0;
@@ -105,6 +105,8 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         H = G.H;
         W = G.W;
         HW = H * W;
+        ylo = G.yhi ? G.ylo : 0;  // rows the taps may read: [0, H), or a row band's halo too
+        yspan = (G.yhi ? G.yhi : H) - ylo;
         npix = G.npix;
         Wo = W >> 1;
         HWo = (H >> 1) * Wo;
@@ -117,7 +119,10 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         if (tid < MT) s_bias[tid] = (m0 + tid < G.cout) ? G.bias[m0 + tid] : 0.f;
 
         // the lane's im2col pixel (run jw): byte offset of its unit in group 0, plane 0
-        const uint8_t* in_base = G.in + (size_t)G.in_l.o0 * 16;
+        // (a row band's view starts its buffer resource 3 rows + 3 units early, so the halo
+        // taps above the band keep non-negative offsets)
+        const uint32_t hshift = G.yhi ? 3u * G.in_l.rs + 3u : 0u;
+        const uint8_t* in_base = G.in + (size_t)(G.in_l.o0 - hshift) * 16;
         int py, px;
         uint32_t pbase;
         {
@@ -128,7 +133,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             const int y = r / W;
             px = r - y * W;
             py = v ? y : -100000;
-            pbase = (n * G.in_l.fs + (uint32_t)y * G.in_l.rs + (uint32_t)px) * 16u;
+            pbase = (n * G.in_l.fs + (uint32_t)y * G.in_l.rs + (uint32_t)px + hshift) * 16u;
         }
 
         AccT acc[TM][TN];
@@ -143,7 +148,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             const int ky = tap / ks;
             const int dy = ky - a.pad, dx = tap - ky * ks - a.pad;
             const int iy = py + dy, ix = px + dx;
-            const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+            const bool ok = (unsigned)(iy - ylo) < (unsigned)yspan && (unsigned)ix < (unsigned)W;
             return ok ? pbase + (uint32_t)((dy * (int)G.in_l.rs + dx) * 16) : 0x80000000u;  // >= num_records -> 0
         };
         // im2col DMA of chunk c, unit u of this wave ((piece, group) row pg0 + u * WPJ) into stage buf;
@@ -594,6 +599,33 @@ void launch_x6p_clear_pads(uint8_t* const* bufs, const int* planes, int nbufs, i
     const size_t pads = ((size_t)(3 * N + 4) * P + (size_t)N * H * 3) * most;
     hipLaunchKernelGGL(x6p_clear_pads_kernel, dim3(std::min(grid_for(pads), 2048), nbufs), dim3(256), 0, st, b, plane,
                        N, H, P);
+}
+
+// Halo rows of a row band (engine.cpp band_halo): 3 consecutive rows of groups [g0, g0 + ng) of
+// each piece plane of a one-frame X6P buffer <-> a packed [piece][group][3 P] unit block.
+// blockIdx.y = direction d (0: the band's top edge, 1: its bottom edge), skipped unless bit d of
+// mask; row[d]: the padded row (3 + y) of the block's first row.
+__global__ __launch_bounds__(256) void x6p_halo_kernel(uint8_t* __restrict__ x6p, uint32_t ps, uint32_t gs, int g0,
+                                                       int ng, int P, int row0, int row1, uint4* __restrict__ blk0,
+                                                       uint4* __restrict__ blk1, int mask, int unpack) {
+    const int d = blockIdx.y;
+    if (!((mask >> d) & 1)) return;
+    uint4* blk = d ? blk1 : blk0;
+    const uint32_t row = (uint32_t)(d ? row1 : row0), per = 3u * (uint32_t)P, total = 3u * (uint32_t)ng * per;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const uint32_t pg = e / per, u = e - pg * per, pc = pg / (uint32_t)ng, g = pg - pc * (uint32_t)ng;
+        uint4* x = reinterpret_cast<uint4*>(x6p + (size_t)pc * ps) + (size_t)(g0 + g) * gs + (size_t)row * P + u;
+        if (unpack) *x = blk[e];
+        else blk[e] = *x;
+    }
+}
+
+void launch_x6p_halo(uint8_t* x6p, uint32_t ps, uint32_t gs, int g0, int ng, int P, int row0, int row1, void* blk0,
+                     void* blk1, int mask, bool unpack, hipStream_t st) {
+    if (!mask) return;
+    const size_t total = (size_t)9 * ng * P;
+    hipLaunchKernelGGL(x6p_halo_kernel, dim3(std::min(grid_for(total), 1024), 2), dim3(256), 0, st, x6p, ps, gs, g0,
+                       ng, P, row0, row1, static_cast<uint4*>(blk0), static_cast<uint4*>(blk1), mask, unpack ? 1 : 0);
 }
 
 // fp32 NCHW channels [coff, coff + C) of cstride -> X6 groups [goff, goff + ceil(C/8)) of cg

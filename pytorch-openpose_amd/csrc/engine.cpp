@@ -263,6 +263,10 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_CONV12_WIN");
         return !(e && e[0] == '0');
     }();
+    // row-band stages (opose_body_band_maps): 0 off; 1: every 3x3 / 7x7 on the window kernel
+    // (it reads the halo rows the band exchange writes; conv_x6 bounds rows to the band);
+    // 2: the same on whole data-parallel tiles (OPOSE_BAND_DP)
+    int band_win = 0;
     DevBuf frames, mids[2][kMaxScales], avg, cnt, list, peak_pos, part_cnt, score, conn, conn_cnt, records, maps_in,
         hlab, hsums, hpeaks, hfound, list_score, hsel;
     PinnedBuf hand_out;  // Hand() peaks + found, staged for the host
@@ -683,6 +687,7 @@ struct XAct {  // a group slice of an X6 buffer (or, f32: a channel slice of an 
     X6Layout l{};        // X6 unit addressing (common.h)
     bool f32 = false;
     bool padded = false;
+    int ylo = 0, yhi = 0;  // X6P row-band view: rows conv taps may read (yhi == 0: the frame's)
 };
 
 static XAct f32act(float* p, int c, int off) {
@@ -835,6 +840,9 @@ static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, boo
         G.H = sg.H;
         G.W = sg.W;
         G.npix = pool ? sg.N * (sg.H / 2) * (sg.W / 2) * 4 : sg.N * sg.H * sg.W;
+        G.ylo = sg.in.ylo;
+        G.yhi = sg.in.yhi;
+        if (G.yhi && (sg.N != 1 || pool)) throw std::invalid_argument("row band views: one frame, no pooling");
         gpix.push_back(G.npix);
         npix_all += G.npix;
         flops += 2.0 * c->cout * (double)c->K * (pool ? 4.0 * sg.N * (sg.H / 2) * (sg.W / 2) : (double)G.npix);
@@ -862,6 +870,17 @@ static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, boo
         if (tiles >= 192 && fill >= 0.85) {
             t = TileChoice{128, 256, (int)tiles};
             kind = "win";
+        }
+    }
+    if (h->band_win == 2) {  // OPOSE_BAND_DP: whole tiles, the same per-pixel sum in any band
+        long tiles = 0;
+        if (win_ok) {
+            for (int n : gpix) tiles += (long)(a.Mpad / 128) * ((n + 255) / 256);
+            t = TileChoice{128, 256, (int)tiles};
+            kind = "win";
+        } else {
+            t = choose_tile(a.Mpad, gpix, a.nK, true, true, &cost);
+            kind = "x6";
         }
     }
     a.sk_grid = t.grid;
@@ -1176,9 +1195,27 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
     }
 }
 
+// Output rows [r0, r1) of one frame's CPM stages (opose_body_band_maps).  The stage buffers keep
+// the whole frame's geometry; every stage layer runs on a view of the band's rows (X6P origin
+// moved down r0 rows), whose padding rows are the neighbouring bands' rows: band_halo refreshes
+// them before each 3x3 / 7x7 layer that reads them.  The trunk before the stages runs whole.
+struct Band {
+    int r0, r1;
+    float* maps;  // [57][r1 - r0][wl] fp32 device
+    opose_halo_fn fn;
+    void* user;
+    uint8_t* xbuf;  // [send_up | send_dn | recv_up | recv_dn], cap bytes each
+    size_t cap;
+};
+
+// bytes of one direction of a band's halo exchange at wl columns: 3 pieces x 32 groups (the
+// widest stage tensor, 256 channels) x 3 rows x (wl + 3) units x 16 B
+static size_t band_halo_bytes(int wl) { return (size_t)3 * 32 * 3 * (wl + 3) * 16; }
+
 // bodypose_model.forward on X6 activations, every segment in lockstep; per segment the fp32
-// output in its slot's S0 with the fp32 path's layout (channel stride 185: paf [0,38), heat [38,57))
-static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& segs) {
+// output in its slot's S0 with the fp32 path's layout (channel stride 185: paf [0,38), heat [38,57)).
+// band: one segment of one frame, stages on rows [band->r0, band->r1) only, output in band->maps.
+static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& segs, const Band* band = nullptr) {
     const int SG = 24, TG = 32, UG = 128;  // [L1 | L2 | trunk] = 5 + 3 + 16 groups; 256 / 1024 channels
     const int net = OPOSE_NET_BODY;
     const size_t ns = segs.size();
@@ -1208,9 +1245,43 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
         last.push_back(x6pact(b.S[0], SG, 8, b.N, b.hl, b.wl));
         dup.push_back(x6pact(b.S[1], SG, 8, b.N, b.hl, b.wl));
     }
-    auto s_ = [&](size_t i, int k, int goff) { return x6pact(bs[i].S[k], SG, goff, bs[i].N, bs[i].hl, bs[i].wl); };
-    auto t_ = [&](size_t i, int k, int goff) { return x6pact(bs[i].T[k], TG, goff, bs[i].N, bs[i].hl, bs[i].wl); };
-    auto u_ = [&](size_t i, int goff) { return x6act(bs[i].U, UG, goff, bs[i].N, bs[i].hl, bs[i].wl); };
+    if (band && (ns != 1 || bs[0].N != 1 || band->r0 < 0 || band->r1 > bs[0].hl || band->r1 - band->r0 < 3))
+        throw std::invalid_argument("row band: one frame, 3 <= r1 - r0 rows inside the map");
+    // rows a stage layer computes, and the band view of a full-height X6P activation
+    const int hb = band ? band->r1 - band->r0 : 0;
+    auto rows = [&](size_t i) { return band ? hb : bs[i].hl; };
+    auto bview = [&](XAct a) {
+        if (band) {
+            a.l.o0 += (uint32_t)band->r0 * a.l.rs;
+            a.l.fs = (uint32_t)(hb + 3) * a.l.rs;
+            a.ylo = band->r0 > 0 ? -3 : 0;
+            a.yhi = band->r1 < bs[0].hl ? hb + 3 : hb;
+        }
+        return a;
+    };
+    auto s_ = [&](size_t i, int k, int goff) { return bview(x6pact(bs[i].S[k], SG, goff, bs[i].N, bs[i].hl, bs[i].wl)); };
+    auto t_ = [&](size_t i, int k, int goff) { return bview(x6pact(bs[i].T[k], TG, goff, bs[i].N, bs[i].hl, bs[i].wl)); };
+    auto u_ = [&](size_t i, int goff) { return x6act(bs[i].U, UG, goff, bs[i].N, rows(i), bs[i].wl); };
+    // band edges: send the band's first / last 3 rows of groups [g0, g0 + ng) of X6P buffer buf
+    // (cg groups) up / down, receive the neighbours' rows into the rows above / below the band
+    auto band_halo = [&](uint8_t* buf, int cg, int g0, int ng) {
+        if (!band) return;
+        const int hl = bs[0].hl, P = bs[0].wl + 3;
+        const size_t plane = x6p_plane(1, hl, bs[0].wl), bytes = (size_t)9 * ng * P * 16;
+        const int mask = (band->r0 > 0 ? 1 : 0) | (band->r1 < hl ? 2 : 0);
+        if (!mask) return;
+        if (bytes > band->cap) throw std::invalid_argument("row band: halo buffer too small");
+        const uint32_t ps = checked_ps((size_t)cg * plane * 16);
+        uint8_t* x = band->xbuf;
+        const size_t c = band->cap;
+        ProfEntry pe;
+        h->prof_begin(pe, "band_halo", 0, 4.0 * (double)bytes);
+        launch_x6p_halo(buf, ps, (uint32_t)plane, g0, ng, P, 3 + band->r0, band->r1, x, x + c, mask, false, h->stream);
+        if (band->fn(band->user, bytes, h->stream) != 0) throw std::runtime_error("row band: halo exchange failed");
+        launch_x6p_halo(buf, ps, (uint32_t)plane, g0, ng, P, band->r0, 3 + band->r1, x + 2 * c, x + 3 * c, mask, true,
+                        h->stream);
+        h->prof_end(pe);
+    };
     // one layer over every segment: branch L1 (conv c1) and, when c2, branch L2
     auto layer = [&](const std::string& n1, const std::string& n2, const std::function<XAct(size_t)>& in1,
                      const std::function<XAct(size_t)>& out1, const std::function<XAct(size_t)>& in2,
@@ -1219,18 +1290,26 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
         DevConv* c2 = n2.empty() ? nullptr : find_conv(h, net, n2);
         std::vector<ConvSeg> cs;
         for (size_t i = 0; i < ns; ++i) {
-            cs.push_back(ConvSeg{c1, bs[i].N, bs[i].hl, bs[i].wl, in1(i), out1(i), XAct{}, relu1});
-            if (c2) cs.push_back(ConvSeg{c2, bs[i].N, bs[i].hl, bs[i].wl, in2(i), out2(i), XAct{}, relu2});
+            cs.push_back(ConvSeg{c1, bs[i].N, rows(i), bs[i].wl, in1(i), out1(i), XAct{}, relu1});
+            if (c2) cs.push_back(ConvSeg{c2, bs[i].N, rows(i), bs[i].wl, in2(i), out2(i), XAct{}, relu2});
         }
         run_conv_x6_segs(h, cs);
     };
     auto none = [](size_t) { return XAct{}; };
     run_trunk_x6(h, net, segs, last, dup);
+    // from here on, a band's convs read halo rows: window kernel only (opose_ctx::band_win)
+    struct BandWin {
+        opose_ctx* h;
+        ~BandWin() { h->band_win = 0; }
+    } band_win_reset{h};
+    if (band) h->band_win = h->band_win ? h->band_win : 1;
     layer("conv5_1_CPM_L1+L2", "", [&](size_t i) { return s_(i, 0, 8); }, [&](size_t i) { return t_(i, 0, 0); }, none,
           none, true, false);
+    band_halo(bs[0].T[0], TG, 0, TG);
     layer("conv5_2_CPM_L1", "conv5_2_CPM_L2", [&](size_t i) { return t_(i, 0, 0); },
           [&](size_t i) { return t_(i, 1, 0); }, [&](size_t i) { return t_(i, 0, 16); },
           [&](size_t i) { return t_(i, 1, 16); }, true, true);
+    band_halo(bs[0].T[1], TG, 0, TG);
     layer("conv5_3_CPM_L1", "conv5_3_CPM_L2", [&](size_t i) { return t_(i, 1, 0); },
           [&](size_t i) { return t_(i, 0, 0); }, [&](size_t i) { return t_(i, 1, 16); },
           [&](size_t i) { return t_(i, 0, 16); }, true, true);
@@ -1248,9 +1327,10 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
     };
     chain("conv5_4_CPM_L1", "conv5_5_CPM_L1", "conv5_4_CPM_L2", "conv5_5_CPM_L2",
           [&](size_t i, int br, DevConv* c1, DevConv* c2) {
-              return ChainSeg{c1, c2, bs[i].N, bs[i].hl, bs[i].wl, t_(i, 0, br ? 16 : 0), u_(i, br ? 64 : 0),
+              return ChainSeg{c1, c2, bs[i].N, rows(i), bs[i].wl, t_(i, 0, br ? 16 : 0), u_(i, br ? 64 : 0),
                               s_(i, 1, br ? 5 : 0), false};
           });
+    band_halo(bs[0].S[1], SG, 0, 8);
     int cur = 1;
     for (int st = 2; st <= 6; ++st) {
         const std::string sf = "_stage" + std::to_string(st);
@@ -1258,6 +1338,7 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
               [&](size_t i) { return t_(i, 0, 0); }, none, none, true, false);
         int t = 0;
         for (int k = 2; k <= 5; ++k) {
+            band_halo(bs[0].T[t], TG, 0, TG);  // Mconv2..5 read 3 rows past the band
             const std::string nm = "Mconv" + std::to_string(k) + sf;
             layer(nm + "_L1", nm + "_L2", [&](size_t i) { return t_(i, t, 0); },
                   [&](size_t i) { return t_(i, t ^ 1, 0); }, [&](size_t i) { return t_(i, t, 16); },
@@ -1268,10 +1349,12 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
         // src/model.py:30-33)
         chain("Mconv6" + sf + "_L1", "Mconv7" + sf + "_L1", "Mconv6" + sf + "_L2", "Mconv7" + sf + "_L2",
               [&](size_t i, int br, DevConv* c1, DevConv* c2) {
-                  const XAct o = st == 6 ? f32act(bs[i].O, 185, br ? 38 : 0) : s_(i, cur ^ 1, br ? 5 : 0);
-                  return ChainSeg{c1, c2, bs[i].N, bs[i].hl, bs[i].wl, t_(i, t, br ? 16 : 0), t_(i, t ^ 1, br ? 16 : 0), o,
+                  const XAct o = st < 6 ? s_(i, cur ^ 1, br ? 5 : 0)
+                                 : band ? f32act(band->maps, 57, br ? 38 : 0) : f32act(bs[i].O, 185, br ? 38 : 0);
+                  return ChainSeg{c1, c2, bs[i].N, rows(i), bs[i].wl, t_(i, t, br ? 16 : 0), t_(i, t ^ 1, br ? 16 : 0), o,
                                   br == 1 && st == 6};
               });
+        if (st < 6) band_halo(bs[0].S[cur ^ 1], SG, 0, 8);  // the next Mconv1 (7x7) reads them
         cur ^= 1;
     }
     std::vector<float*> outs;
@@ -2203,6 +2286,45 @@ int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, i
                                                                     : hipMemcpyDeviceToHost,
                                          h->stream));
         if (!(flags & OPOSE_OUT_DEVICE)) OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+        return OPOSE_OK;
+    });
+}
+
+size_t opose_body_band_halo_bytes(int wl) { return wl > 0 ? band_halo_bytes(wl) : 0; }
+
+int opose_body_band_maps(opose_t* h, const uint8_t* bgr, int H, int W, int64_t row_stride, const opose_params* pp,
+                         int s, int r0, int r1, float* maps, opose_halo_fn fn, void* user, void* xbuf,
+                         size_t xbuf_bytes, int flags) {
+    if (!h || !bgr || !maps || !fn || !xbuf || H <= 0 || W <= 0 || row_stride < (int64_t)W * 3) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        enter_main(h);
+        const opose_params p = fill_params(pp, OPOSE_NET_BODY);
+        if (s < 0 || s >= p.n_scales) return OPOSE_E_ARG;
+        const ScaleGeom g = geom(p.scales[s], p, H, W);
+        if (r0 < 0 || r1 > g.hl || r1 - r0 < 3) return OPOSE_E_ARG;
+        if (xbuf_bytes < 4 * band_halo_bytes(g.wl)) return OPOSE_E_ARG;
+        if (!h->x6) throw std::invalid_argument("row bands need the split-bf16 path (OPOSE_CONV=f32 is set)");
+        if (!h->loaded[OPOSE_NET_BODY]) throw std::runtime_error("body weights not loaded");
+        const uint8_t* fd = bgr;
+        if (!(flags & OPOSE_IN_DEVICE)) {
+            uint8_t* buf = h->frames.ensure<uint8_t>((size_t)row_stride * H, h->stream);
+            OPOSE_HIP_CHECK(hipMemcpyAsync(buf, bgr, host_span(1, H, W, row_stride, row_stride * H),
+                                           hipMemcpyHostToDevice, h->stream));
+            fd = buf;
+        }
+        const int hb = r1 - r0;
+        float* out = (flags & OPOSE_OUT_DEVICE) ? maps : h->maps_in.ensure<float>((size_t)57 * hb * g.wl, h->stream);
+        float* x = h->w().x.ensure<float>((size_t)3 * g.Hp * g.Wp, h->stream);
+        launch_preprocess(fd, row_stride * H, row_stride, 1, H, W, g.Hs, g.Ws, 1.0 / g.mult, 1.0 / g.mult, g.Hp, g.Wp,
+                          (float)p.pad_value / 256.f - 0.5f, x, h->stream);
+        const size_t cap = xbuf_bytes / 4;
+        const Band band{r0, r1, out, fn, user, static_cast<uint8_t*>(xbuf), cap};
+        h->band_win = (flags & OPOSE_BAND_DP) ? 2 : 1;
+        body_net_x6(h, {NetSeg{x, 1, g.Hp, g.Wp, h->slot}}, &band);
+        if (!(flags & OPOSE_OUT_DEVICE)) {
+            OPOSE_HIP_CHECK(hipMemcpyAsync(maps, out, (size_t)57 * hb * g.wl * 4, hipMemcpyDeviceToHost, h->stream));
+            OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
+        }
         return OPOSE_OK;
     });
 }

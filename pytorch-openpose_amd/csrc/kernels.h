@@ -43,6 +43,11 @@ void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const fl
                           uint8_t* out, uint32_t ops, bool f32_out, hipStream_t st);
 // zero the padding units of `planes` X6P (piece, group) planes of an N x H x W buffer (common.h)
 void launch_x6p_clear_pads(uint8_t* const* bufs, const int* planes, int nbufs, int N, int H, int W, hipStream_t st);
+// 3 rows (padded row index row0 / row1) of groups [g0, g0 + ng) of a one-frame X6P buffer (ps
+// bytes per piece, gs units per group plane, P units per row) <-> packed blocks blk0 / blk1
+// ([piece][group][3 P] units); directions by mask bit 0 / 1
+void launch_x6p_halo(uint8_t* x6p, uint32_t ps, uint32_t gs, int g0, int ng, int P, int row0, int row1, void* blk0,
+                     void* blk1, int mask, bool unpack, hipStream_t st);
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,
                        hipStream_t st);
 // conv1_2 (64 -> 64, 3x3 pad 1) + MaxPool2d(2, 2) from an 8-group X6 tensor (f32_in: fp32 units,

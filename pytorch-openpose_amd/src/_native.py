@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("OPOSE_LIB", os.path.join(os.path.dirname(_HERE), "lib
 OPOSE_OK = 0
 OPOSE_E_ARG, OPOSE_E_SHAPE, OPOSE_E_HIP, OPOSE_E_WEIGHTS, OPOSE_E_CAPACITY, OPOSE_E_ASSEMBLY = -1, -2, -3, -4, -5, -6
 NET_BODY, NET_HAND = 0, 1
-IN_DEVICE, OUT_DEVICE, PIPELINE = 1, 2, 4
+IN_DEVICE, OUT_DEVICE, PIPELINE, BAND_DP = 1, 2, 4, 8
 MAX_SCALES = 8
 
 
@@ -24,6 +24,10 @@ class Params(C.Structure):
     _fields_ = [("n_scales", C.c_int), ("scales", C.c_double * MAX_SCALES), ("boxsize", C.c_double),
                 ("stride", C.c_int), ("pad_value", C.c_int), ("thre1", C.c_double), ("thre2", C.c_double),
                 ("thre_hand", C.c_double)]
+
+
+# int (*opose_halo_fn)(void* user, size_t bytes, void* stream)
+HALO_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_size_t, C.c_void_p)
 
 
 def _load():
@@ -53,6 +57,8 @@ def _load():
         "opose_body_scale_geom": (I, [I, I, C.POINTER(Params), I, P]),
         "opose_body_scale_maps": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), I, P, I]),
         "opose_body_post_scales": (I, [P, C.POINTER(P), P, P, P, P, I, I, I, I, C.POINTER(Params), P, I]),
+        "opose_body_band_halo_bytes": (S, [I]),
+        "opose_body_band_maps": (I, [P, P, I, I, C.c_int64, C.POINTER(Params), I, I, I, P, HALO_FN, P, P, S, I]),
         "opose_hand_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, P, I]),
         "opose_hand_post": (I, [P, C.POINTER(P), P, P, P, P, I, I, I, I, C.POINTER(Params), P, P, I]),
         "opose_hand_infer_crops": (I, [P, C.POINTER(P), P, P, I, C.POINTER(Params), P, P, I]),
@@ -89,7 +95,7 @@ EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last
             "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_hand_forward_pyramid",
             "opose_body_infer",
             "opose_body_post", "opose_body_scale_geom", "opose_body_scale_maps",
-            "opose_body_post_scales", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
+            "opose_body_post_scales", "opose_body_band_halo_bytes", "opose_body_band_maps", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
             "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_conv_time", "opose_debug_conv_x6", "opose_debug_conv_x6_time", "opose_debug_preprocess",
             "opose_debug_heat", "opose_debug_hand_label"]
 

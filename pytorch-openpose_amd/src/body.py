@@ -136,6 +136,65 @@ class Body(object):
             maps.ctypes.data, 0))
         return maps
 
+    def band_maps(self, frame, s, r0, r1, exchange=None, exact=False):
+        """Rows [r0, r1) of scale `s`'s network maps for one frame: [1, 57, r1-r0, wl] float32
+        (opose_body_band_maps; src/body.py:36-50 for one m, cut into output rows).
+
+        frame: uint8 [H,W,3] numpy (-> numpy) or torch cuda tensor (-> torch cuda tensor in
+        torch's current-stream order).  exchange(xbuf, cap, nbytes, stream) moves the halo rows
+        between neighbouring bands (src.dist.band_exchange): xbuf is the uint8 device tensor
+        [send_up | send_dn | recv_up | recv_dn] of `cap` bytes each, `stream` the library's
+        hipStream_t, on which the send halves are being packed.  Not needed when one band covers
+        every row.  exact: whole data-parallel tiles (bit-identical to any other banding)."""
+        import torch
+        dev = hasattr(frame, "data_ptr")
+        if dev:
+            frame = frame[0] if frame.dim() == 4 else frame
+            if frame.stride(1) != 3 or frame.stride(2) != 1:
+                raise ValueError("expected a uint8 frame [H, W, 3] with packed pixels")
+            H, W, _ = frame.shape
+            ptr, rs = frame.data_ptr(), frame.stride(0)
+        else:
+            frame = np.ascontiguousarray(np.asarray(frame)[0] if np.ndim(frame) == 4 else frame)
+            H, W, _ = frame.shape
+            ptr, rs = frame.ctypes.data, frame.strides[0]
+        hl, wl, _, _ = self.scale_geom(H, W)[s]
+        cap = int(_native.lib.opose_body_band_halo_bytes(wl))
+        xbuf = torch.empty(4 * cap, dtype=torch.uint8, device=torch.device("cuda", self.handle.device))
+        err = []
+
+        def _cb(user, nbytes, stream):
+            try:
+                if exchange is None:
+                    raise RuntimeError("row band with neighbours but no exchange")
+                exchange(xbuf, cap, int(nbytes), stream)
+                return 0
+            except BaseException as e:  # reported after the call returns
+                err.append(e)
+                return 1
+
+        cb = _native.HALO_FN(_cb)
+        flags = _native.BAND_DP if exact else 0
+        if dev:
+            out = torch.empty((1, 57, r1 - r0, wl), dtype=torch.float32, device=frame.device)
+            self.handle.wait_torch()
+            rc = _native.lib.opose_body_band_maps(self.handle.h, ptr, H, W, rs, self.params, s, r0, r1,
+                                                  out.data_ptr(), cb, None, xbuf.data_ptr(), xbuf.numel(),
+                                                  flags | _native.IN_DEVICE | _native.OUT_DEVICE)
+            if err:
+                raise err[0]
+            self.handle.check(rc)
+            self.handle.signal_torch()
+            return out
+        self.handle.wait_torch()  # xbuf was allocated on torch's stream
+        out = np.empty((1, 57, r1 - r0, wl), np.float32)
+        rc = _native.lib.opose_body_band_maps(self.handle.h, ptr, H, W, rs, self.params, s, r0, r1, out.ctypes.data,
+                                              cb, None, xbuf.data_ptr(), xbuf.numel(), flags)
+        if err:
+            raise err[0]
+        self.handle.check(rc)
+        return out
+
     def post_scales(self, maps, H, W):
         """Multi-scale post-network path (src/body.py:51-212): maps[s] = [N,57,hl,wl] for every
         scale of scale_search (numpy, or torch cuda tensors) -> list of (candidate, subset)."""

@@ -78,13 +78,97 @@ def scale_plan(costs, world: int):
     return owner
 
 
-def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=None):
+# ---- balanced split: the largest scales cut into row bands (opose_body_band_maps)
+# Scales are whole networks, so longest-first assignment leaves the 2.0 scale (53 % of the
+# pyramid) alone on one rank.  A scale can instead be cut into nb row bands on nb ranks: each
+# band rank runs the VGG trunk on the whole scale (TRUNK_FRAC of its FLOPs: 602 k of 2.007 M
+# FLOPs per network-input pixel, src/model.py:7-49 against 106-133) and the CPM stages on its
+# own rows, exchanging 3 halo rows with its neighbours before each 3x3 / 7x7 stage layer.
+TRUNK_FRAC = 0.30
+BAND_OVERHEAD = 0.03  # per banded piece, fraction of the scale: 27 halo exchanges, lower grid fill
+MIN_BAND_ROWS = 8
+
+
+def band_rows(hl: int, nb: int):
+    """Contiguous [r0, r1) output rows of each of nb bands of an hl-row map."""
+    return [(hl * i // nb, hl * (i + 1) // nb) for i in range(nb)]
+
+
+def split_plan(costs, world: int, hls=None, trunk_frac: float = TRUNK_FRAC, overhead: float = BAND_OVERHEAD):
+    """Balanced single-frame split of a scale pyramid over `world` ranks.
+
+    costs[s]: work of scale s (~ hl * wl); hls[s]: its output rows (bands keep >= MIN_BAND_ROWS).
+    Returns (order, owners, load): owners[s] = ranks of scale s's bands, top to bottom (one rank:
+    the whole scale); every rank runs its pieces in `order` (scales by decreasing piece cost, the
+    same order everywhere, so the band groups' halo exchanges cannot wait on each other in a
+    cycle); load[r] = modelled work of rank r.  Exhaustive over band counts (world^n_scales
+    combinations, <= 4096 at 8 ranks and 4 scales), pieces placed largest-first on the least
+    loaded distinct ranks; ties keep fewer bands."""
+    import itertools
+    ns = len(costs)
+    hls = hls if hls is not None else [10 ** 9] * ns
+    best = None
+    choices = [[nb for nb in range(1, world + 1) if nb == 1 or hls[s] // nb >= MIN_BAND_ROWS] for s in range(ns)]
+    for nbs in itertools.product(*choices):
+        piece = [costs[s] * (1.0 if nbs[s] == 1 else trunk_frac + (1 - trunk_frac) / nbs[s] + overhead)
+                 for s in range(ns)]
+        order = sorted(range(ns), key=lambda i: (-piece[i], i))
+        load = [0.0] * world
+        owners = [None] * ns
+        for s in order:
+            ranks = sorted(range(world), key=lambda k: (load[k], k))[:nbs[s]]
+            owners[s] = sorted(ranks)
+            for r in ranks:
+                load[r] += piece[s]
+        key = (round(max(load), 9), sum(nbs))
+        if best is None or key < best[0]:
+            best = (key, order, owners, load)
+    return best[1], best[2], best[3]
+
+
+def band_exchange(rank_up, rank_dn, group=None):
+    """Halo exchange of one band for Body.band_maps: send_up -> the band above (rank_up), send_dn
+    -> the band below (rank_dn), their rows into recv_up / recv_dn.  RCCL ('nccl'): device
+    P2P ops ordered on the library's stream; gloo: through host memory, synchronously."""
+    def ex(xbuf, cap, n, stream):
+        pairs = [(r, o) for r, o in ((rank_up, 0), (rank_dn, 1)) if r is not None]
+        if dist.get_backend(group) == "nccl":
+            with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=xbuf.device)):
+                ops = []
+                for r, o in pairs:
+                    ops.append(dist.P2POp(dist.isend, xbuf[o * cap:o * cap + n], r, group))
+                    ops.append(dist.P2POp(dist.irecv, xbuf[(2 + o) * cap:(2 + o) * cap + n], r, group))
+                for q in dist.batch_isend_irecv(ops):
+                    q.wait()
+            return
+        if xbuf.is_cuda:
+            torch.cuda.ExternalStream(stream, device=xbuf.device).synchronize()  # send halves packed
+        host = xbuf[:2 * cap].cpu()
+        recv = {o: torch.empty(n, dtype=torch.uint8) for _, o in pairs}
+        reqs = []
+        for r, o in pairs:
+            reqs.append(dist.isend(host[o * cap:o * cap + n].clone(), r, group=group))
+            reqs.append(dist.irecv(recv[o], r, group=group))
+        for q in reqs:
+            q.wait()
+        for _, o in pairs:
+            xbuf[(2 + o) * cap:(2 + o) * cap + n].copy_(recv[o])
+        if xbuf.is_cuda:
+            torch.cuda.current_stream(xbuf.device).synchronize()  # before the library unpacks them
+    return ex
+
+
+def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=None, split: str = "balanced"):
     """Body(frame) with its scales split across ranks; returns [(candidate, subset)] on `dst`
     (None elsewhere).  frame: uint8 [H,W,3] / [1,H,W,3] numpy, or a torch cuda tensor (then the
     maps stay on the device and travel over RCCL; with gloo they go through host memory).
 
-    Result: identical to body.batch(frame) on one GPU — each scale's network runs with the same
-    shapes (so the same kernels and summation order) and the post path is the same code."""
+    split="scales": whole scales, longest first (scale_plan).  Result identical to
+    body.batch(frame) on one GPU: each scale's network runs with the same shapes (so the same
+    kernels and summation order) and the post path is the same code.
+    split="balanced" (default): split_plan, which may cut the largest scales into row bands
+    (Body.band_maps).  Where it keeps every scale whole the result is the same as "scales";
+    banded scales match the one-GPU maps to fp32 summation order (the conv grids differ)."""
     import numpy as np
     dev = hasattr(frame, "data_ptr")
     if not dev:
@@ -96,33 +180,52 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
             frame = frame[None]
     N, H, W, _ = frame.shape
     geoms = body.scale_geom(H, W)
-    owner = scale_plan([g[0] * g[1] for g in geoms], world)
+    costs = [g[0] * g[1] for g in geoms]
+    if split == "scales" or N != 1:
+        order = list(range(len(geoms)))
+        owners = [[r] for r in scale_plan(costs, world)]
+    elif split == "balanced":
+        order, owners, _ = split_plan(costs, world, [g[0] for g in geoms])
+    else:
+        raise ValueError("split must be 'balanced' or 'scales'")
     on_device = dev and dist.get_backend(group) == "nccl"
-    maps = [None] * len(geoms)
-    for s, r in enumerate(owner):
-        if r != rank:
+    local = frame if on_device else (frame.cpu().numpy() if dev else frame)
+    pieces = {}  # (s, band) -> maps of this rank
+    for s in order:
+        if rank not in owners[s]:
             continue
-        if on_device:
-            maps[s] = body.scale_maps(frame, s)
+        if len(owners[s]) == 1:
+            m = body.scale_maps(local, s)
         else:
-            host = body.scale_maps(frame.cpu().numpy() if dev else frame, s)
-            maps[s] = torch.from_numpy(host)
-    if world > 1:
-        reqs = []
-        for s, r in enumerate(owner):
-            if r == dst and rank == dst:
-                continue
-            if rank == r:
-                reqs.append(dist.isend(maps[s].contiguous(), dst, group=group))
+            b = owners[s].index(rank)
+            r0, r1 = band_rows(geoms[s][0], len(owners[s]))[b]
+            up = owners[s][b - 1] if b > 0 else None
+            dn = owners[s][b + 1] if b + 1 < len(owners[s]) else None
+            m = body.band_maps(local[0], s, r0, r1, band_exchange(up, dn, group))
+        pieces[(s, owners[s].index(rank))] = m if on_device else torch.from_numpy(m)
+    maps = [None] * len(geoms)
+    reqs = []
+    for s in range(len(geoms)):
+        nb = len(owners[s])
+        rows = band_rows(geoms[s][0], nb)
+        parts = []
+        for b, r in enumerate(owners[s]):
+            if r == rank and (rank == dst or world == 1):
+                parts.append(pieces[(s, b)])
+            elif rank == r:
+                reqs.append(dist.isend(pieces[(s, b)].contiguous(), dst, group=group))
             elif rank == dst:
-                hl, wl = geoms[s][0], geoms[s][1]
-                maps[s] = torch.empty((N, 57, hl, wl), dtype=torch.float32,
-                                      device=frame.device if on_device else "cpu")
-                reqs.append(dist.irecv(maps[s], r, group=group))
-        for q in reqs:
-            q.wait()
+                t = torch.empty((N, 57, rows[b][1] - rows[b][0], geoms[s][1]), dtype=torch.float32,
+                                device=frame.device if on_device else "cpu")
+                reqs.append(dist.irecv(t, r, group=group))
+                parts.append(t)
+        if rank == dst:
+            maps[s] = parts
+    for q in reqs:
+        q.wait()
     if rank != dst:
         return None
+    maps = [p[0] if len(p) == 1 else torch.cat(p, 2) for p in maps]
     if on_device:
         return body.post_scales(maps, H, W)
     return body.post_scales([m.numpy() for m in maps], H, W)

@@ -195,6 +195,35 @@ def main():
         own = scale_plan([g[0] * g[1] for g in geoms], world)
         load = [sum(t for t, r in zip(net_ms, own) if r == k) for k in range(world)]
         out["C5_sharded_w%d_model_ms_excl_gather" % world] = max(load) + post_ms
+    # balanced split (src.dist.split_plan): the largest scales cut into row bands.  A band's time
+    # is measured here with the halo exchange stubbed out (the 27 pack / unpack launches per band
+    # run, the transfer does not); the transfer is modelled as 27 x (10 us + 2 x the halo bytes at
+    # 100 GB/s), the halo bytes being 3 rows x 256 channels x 6 B x (wl + 3) per direction.
+    from src.dist import band_rows, split_plan
+
+    def noop(xbuf, cap, n, stream):
+        return None
+    costs, hls = [g[0] * g[1] for g in geoms], [g[0] for g in geoms]
+    band_ms = {}
+    for world in (2, 4, 8):
+        order, owners, _ = split_plan(costs, world, hls)
+        load = [0.0] * world
+        for s in order:
+            nb = len(owners[s])
+            if nb == 1:
+                t = net_ms[s]
+            else:
+                if (s, nb) not in band_ms:
+                    xfer = 27 * (10e-3 + 2 * 3 * 256 * 6 * (geoms[s][1] + 3) / 100e9 * 1e3)
+                    band_ms[(s, nb)] = max(
+                        timed(lambda r=r: body5.band_maps(f1, s, r[0], r[1], noop), 5, warm=1)
+                        for r in band_rows(geoms[s][0], nb)) + xfer
+                t = band_ms[(s, nb)]
+            for r in owners[s]:
+                load[r] += t
+        out["C5_balanced_w%d_owners" % world] = owners
+        out["C5_balanced_w%d_model_ms_excl_gather" % world] = max(load) + post_ms
+    out["C5_band_ms"] = {"%d/%d" % k: v for k, v in band_ms.items()}
     print(json.dumps(out))
 
 

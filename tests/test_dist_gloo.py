@@ -87,6 +87,7 @@ class _FakeBody:
 
     def __init__(self):
         self.computed = []
+        self.bands = []
 
     def scale_geom(self, H, W):
         return GEOMS
@@ -97,25 +98,49 @@ class _FakeBody:
         rng = np.random.default_rng(100 + s)
         return rng.standard_normal((frame.shape[0], 57, hl, wl)).astype(np.float32)
 
+    def band_maps(self, frame, s, r0, r1, exchange=None, exact=False):
+        """Rows [r0, r1) of scale_maps(s); drives the real halo exchange with a host xbuf whose
+        send halves carry (scale, first row / last row) tags, and checks what comes back."""
+        self.bands.append((s, r0, r1))  # (scale_maps below records s in computed)
+        hl = GEOMS[s][0]
+        cap, n = 64, 40
+        xbuf = torch.zeros(4 * cap, dtype=torch.uint8)
+        xbuf[0:n] = s * 16 + r0 % 16             # my top rows, for the band above
+        xbuf[cap:cap + n] = s * 16 + (r1 - 1) % 16  # my bottom rows, for the band below
+        for _ in range(3):
+            exchange(xbuf, cap, n, None)
+        if r0 > 0:   # the band above sent its last row's tag
+            assert (xbuf[2 * cap:2 * cap + n] == s * 16 + (r0 - 1) % 16).all()
+        if r1 < hl:  # the band below sent its first row's tag
+            assert (xbuf[3 * cap:3 * cap + n] == s * 16 + r1 % 16).all()
+        return self.scale_maps(frame[None], s)[:, :, r0:r1].copy()
+
     def post_scales(self, maps, H, W):
         return [np.asarray(m) for m in maps]
 
 
-def _scale_worker(rank, world, port, q):
+def _scale_worker(rank, world, port, q, split="scales"):
     import sys
     for p in (PKG, REPO):
         if p not in sys.path:
             sys.path.insert(0, p)
-    from src.dist import body_scale_sharded, scale_plan
+    from src.dist import band_rows, body_scale_sharded, scale_plan, split_plan
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         body = _FakeBody()
         frame = np.zeros((90, 160, 3), np.uint8)
-        out = body_scale_sharded(body, frame, rank, world, dst=0)
-        owner = scale_plan([g[0] * g[1] for g in GEOMS], world)
-        ok = sorted(body.computed) == [s for s, r in enumerate(owner) if r == rank]
+        out = body_scale_sharded(body, frame, rank, world, dst=0, split=split)
+        if split == "scales":
+            order, owners = range(len(GEOMS)), [[r] for r in scale_plan([g[0] * g[1] for g in GEOMS], world)]
+        else:
+            order, owners, _ = split_plan([g[0] * g[1] for g in GEOMS], world, [g[0] for g in GEOMS])
+        ok = sorted(body.computed) == [s for s, rs in enumerate(owners) if rank in rs]
+        ok &= body.bands == [(s, *band_rows(GEOMS[s][0], len(owners[s]))[owners[s].index(rank)])
+                             for s in order if rank in owners[s] and len(owners[s]) > 1]
+        if split == "balanced" and world == 4:
+            ok &= any(len(rs) > 1 for rs in owners)  # the test exercises real bands
         if rank == 0:
             ok &= len(out) == len(GEOMS)
             for s, m in enumerate(out):
@@ -127,12 +152,15 @@ def _scale_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_scale_sharded_gathers_lowres_maps(world):
+@pytest.mark.parametrize("world,split", [(2, "scales"), (3, "scales"), (3, "balanced"), (4, "balanced")])
+def test_scale_sharded_gathers_lowres_maps(world, split):
+    """Scale / band sharding on CPU ranks: each rank computes exactly its planned pieces, band
+    neighbours exchange halo rows (src.dist.band_exchange over gloo), and rank 0 reassembles
+    every scale's maps in row order."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29900 + world * 13 + os.getpid() % 200
-    procs = [ctx.Process(target=_scale_worker, args=(r, world, port, q)) for r in range(world)]
+    port = 29900 + world * 13 + (split == "balanced") * 7 + os.getpid() % 200
+    procs = [ctx.Process(target=_scale_worker, args=(r, world, port, q, split)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
@@ -154,3 +182,33 @@ def test_scale_plan_balances_largest_first():
         own = scale_plan(costs, w)
         load = [sum(c for c, r in zip(costs, own) if r == k) for k in range(w)]
         assert max(load) == 4.0
+
+
+def test_split_plan_cuts_the_largest_scale_into_bands():
+    """split_plan (src/dist.py): C5's pyramid (hl x wl = 23x41, 46x82, 69x123, 92x164 at 1080p)
+    over 1 / 2 / 4 / 8 ranks.  Two ranks keep whole scales (then the result stays bit-identical
+    to one GPU); four and eight cut the 2.0 scale (and at eight the 1.5 scale) into row bands,
+    lowering the modelled critical path below the whole 2.0 scale (the longest-first bound)."""
+    import sys
+    sys.path.insert(0, PKG)
+    from src.dist import band_rows, split_plan, TRUNK_FRAC
+    geo = [(23, 41), (46, 82), (69, 123), (92, 164)]
+    costs = [h * w for h, w in geo]
+    hls = [h for h, _ in geo]
+    order, owners, load = split_plan(costs, 1, hls)
+    assert owners == [[0]] * 4 and order == [3, 2, 1, 0]
+    _, owners, load = split_plan(costs, 2, hls)
+    assert all(len(o) == 1 for o in owners) and max(load) == costs[3]
+    _, owners, load = split_plan(costs, 4, hls)
+    assert len(owners[3]) == 2 and max(load) < 0.75 * costs[3]
+    _, owners, load = split_plan(costs, 8, hls)
+    assert len(owners[3]) >= 4 and max(load) < 0.55 * costs[3]
+    assert max(load) > TRUNK_FRAC * costs[3]          # the replicated trunk bounds it
+    for w in (3, 4, 5, 8):
+        order, owners, load = split_plan(costs, w, hls)
+        for s, rs in enumerate(owners):
+            assert len(set(rs)) == len(rs) and all(0 <= r < w for r in rs)
+            if len(rs) > 1:
+                assert min(b - a for a, b in band_rows(hls[s], len(rs))) >= 8
+    rows = band_rows(92, 5)
+    assert rows[0][0] == 0 and rows[-1][1] == 92 and all(a[1] == b[0] for a, b in zip(rows, rows[1:]))

@@ -1,0 +1,166 @@
+"""GPU: row bands of one scale (opose_body_band_maps) — the balanced C5 split (SURVEY.md §8(e):
+"balance them, because 736x1312 is 53 % of FLOPs").
+
+A band rank runs the trunk on the whole scale and the CPM stages (src/model.py:106-133) on its
+own output rows, with 3 halo rows exchanged before every 3x3 / 7x7 stage layer.
+
+* exact bands (OPOSE_BAND_DP: whole data-parallel tiles, one summation order per pixel) put
+  together equal the single whole-height band bit for bit — the halo exchange is lossless;
+* default bands (stream-K grids per band) equal opose_body_scale_maps within the network
+  tolerance of tests/test_gpu_parity.py (fp32 summation order only);
+* body_scale_sharded(split="balanced") with four gloo ranks on cuda:0 (the 2.0 scale cut into two
+  bands) gives Body(frame)'s keypoints and people (north-star bar)."""
+import os
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import PKG, REPO
+
+pytestmark = pytest.mark.gpu
+
+SCALES = (0.5, 1.0, 1.5, 2.0)
+HW = (368, 656)  # the 2.0 scale is C5's largest network: 736 x 1312 -> 92 x 164 maps
+
+
+def _net_tol(gpu, ref):
+    ref = np.asarray(ref)
+    np.testing.assert_allclose(gpu, ref, rtol=2e-4, atol=2e-4 * float(np.abs(ref).max()))
+
+
+@pytest.fixture(scope="module")
+def bodies():
+    from src.body import Body
+    from src.weights import seeded_state_dict
+    sd = seeded_state_dict("body", 0)
+    return [Body(sd, scale_search=SCALES) for _ in range(3)]
+
+
+@pytest.fixture(scope="module")
+def frame():
+    return np.random.default_rng(41).integers(0, 256, HW + (3,), dtype=np.uint8)
+
+
+def _run_bands(bodies, frame, s, rows, exact):
+    """Every band on its own handle and thread; the halo exchange copies device to device
+    between neighbouring bands' xbufs (two barriers: both sides packed / both sides copied)."""
+    nb = len(rows)
+    bar = threading.Barrier(nb)
+    xbufs = [None] * nb
+    out = [None] * nb
+    errs = []
+
+    def exchange_for(b):
+        def ex(xbuf, cap, n, stream):
+            torch.cuda.ExternalStream(stream).synchronize()
+            xbufs[b] = xbuf
+            bar.wait()
+            if b > 0:
+                xbuf[2 * cap:2 * cap + n].copy_(xbufs[b - 1][cap:cap + n])   # above: its bottom rows
+            if b + 1 < nb:
+                xbuf[3 * cap:3 * cap + n].copy_(xbufs[b + 1][0:n])           # below: its top rows
+            torch.cuda.synchronize()
+            bar.wait()
+        return ex
+
+    def run(b):
+        try:
+            r0, r1 = rows[b]
+            out[b] = bodies[b].band_maps(frame, s, r0, r1, exchange_for(b), exact=exact)
+        except BaseException as e:
+            errs.append(e)
+            bar.abort()
+
+    th = [threading.Thread(target=run, args=(b,)) for b in range(nb)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "band threads hung"
+    if errs:
+        raise errs[0]
+    return np.concatenate(out, 2)
+
+
+@pytest.mark.parametrize("s,nb", [(3, 2), (3, 3), (2, 2)])
+def test_exact_bands_equal_whole_band(bodies, frame, s, nb):
+    from src.dist import band_rows
+    hl, wl, _, _ = bodies[0].scale_geom(*HW)[s]
+    whole = bodies[0].band_maps(frame, s, 0, hl, exact=True)
+    assert whole.shape == (1, 57, hl, wl)
+    got = _run_bands(bodies, frame, s, band_rows(hl, nb), exact=True)
+    assert np.array_equal(got, whole)
+    _net_tol(whole, bodies[0].scale_maps(frame, s))
+
+
+def test_default_bands_match_scale_maps(bodies, frame):
+    from src.dist import band_rows
+    s = 3
+    hl = bodies[0].scale_geom(*HW)[s][0]
+    ref = bodies[0].scale_maps(frame, s)
+    got = _run_bands(bodies, frame, s, band_rows(hl, 3), exact=False)
+    assert got.shape == ref.shape
+    _net_tol(got, ref)
+    assert (got[:, 38:] >= 0).all()  # Mconv7_stage6_L2 keeps its ReLU (src/model.py:30-33)
+
+
+def test_band_maps_argument_checks(bodies, frame):
+    from src._native import OposeError
+    hl = bodies[0].scale_geom(*HW)[3][0]
+    with pytest.raises(OposeError):
+        bodies[0].band_maps(frame, 3, 0, 2)           # fewer than 3 rows
+    with pytest.raises(OposeError):
+        bodies[0].band_maps(frame, 3, 10, hl + 1)     # past the map
+    with pytest.raises(RuntimeError):
+        bodies[0].band_maps(frame, 3, 0, 40)          # neighbours but no exchange
+
+
+def _balanced_worker(rank, world, port, q):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from src.body import Body
+    from src.dist import body_scale_sharded, split_plan
+    from src.weights import c5_out_scale, seeded_state_dict
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b = Body(seeded_state_dict("body", 0, out_scale=c5_out_scale()), scale_search=SCALES)
+        img = np.random.default_rng(43).integers(0, 256, HW + (3,), dtype=np.uint8)
+        geo = b.scale_geom(*HW)
+        _, owners, _ = split_plan([g[0] * g[1] for g in geo], world, [g[0] for g in geo])
+        banded = len(owners[3]) > 1
+        out = body_scale_sharded(b, img, rank, world, split="balanced")
+        msg = ""
+        if rank == 0:
+            (cand, subset), = out
+            (rc, rs), = b.batch(img[None])
+            ok = banded and cand.shape == rc.shape and subset.shape == rs.shape and len(cand) > 0
+            ok = ok and np.array_equal(cand[:, [0, 1, 3]], rc[:, [0, 1, 3]])
+            ok = ok and np.allclose(cand[:, 2], rc[:, 2], rtol=1e-3, atol=1e-4)
+            ok = ok and np.array_equal(subset[:, :18], rs[:, :18]) and np.array_equal(subset[:, 19], rs[:, 19])
+            msg = "banded=%s peaks %d/%d people %d/%d" % (banded, len(cand), len(rc), len(subset), len(rs))
+        else:
+            ok = out is None
+        q.put((rank, bool(ok), msg))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_balanced_split_four_ranks_matches_body():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 300
+    procs = [ctx.Process(target=_balanced_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
