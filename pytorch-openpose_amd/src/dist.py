@@ -81,11 +81,20 @@ def scale_plan(costs, world: int):
 # ---- balanced split: the largest scales cut into row bands (opose_body_band_maps)
 # Scales are whole networks, so longest-first assignment leaves the 2.0 scale (53 % of the
 # pyramid) alone on one rank.  A scale can instead be cut into nb row bands on nb ranks: each
-# band rank runs the VGG trunk on the whole scale (TRUNK_FRAC of its FLOPs: 602 k of 2.007 M
-# FLOPs per network-input pixel, src/model.py:7-49 against 106-133) and the CPM stages on its
-# own rows, exchanging 3 halo rows with its neighbours before each 3x3 / 7x7 stage layer.
+# band rank runs the VGG trunk (TRUNK_FRAC of the FLOPs: 602 k of 2.007 M per network-input
+# pixel, src/model.py:7-49 against 106-133) on its rows plus BAND_MARGIN rows past each cut
+# (recomputed, not exchanged: the trunk's receptive field is small) and the CPM stages on its
+# own rows, exchanging 3 halo rows with its neighbours before each 3x3 / 7x7 stage layer (the
+# stages' receptive field, 84 rows at H/8, rules out recomputing theirs).
 TRUNK_FRAC = 0.30
-BAND_OVERHEAD = 0.03  # per banded piece, fraction of the scale: 27 halo exchanges, lower grid fill
+BAND_MARGIN = 10  # output rows (engine.cpp kBandTrunkMargin)
+# per banded piece: a fraction of the scale's work (lower grid fill of the band's smaller
+# layers) plus a fixed latency in output pixels (~0.5 ms: 54 pack / unpack launches, 27 halo
+# callbacks, per-launch costs of the band's ~90 launches); fitted to one MI355X
+# (profiles/r3_bench_configs.json C5_band_ms: 2.0 scale in 3 / 4 bands 4.89 / 4.10 ms against
+# 8.17 whole, 1.5 in 3 bands 3.47 against 5.35, 1.0 in 2 bands 2.61 against 2.72)
+BAND_OVERHEAD = 0.12
+BAND_LATENCY_PX = 900
 MIN_BAND_ROWS = 8
 
 
@@ -97,7 +106,8 @@ def band_rows(hl: int, nb: int):
 def split_plan(costs, world: int, hls=None, trunk_frac: float = TRUNK_FRAC, overhead: float = BAND_OVERHEAD):
     """Balanced single-frame split of a scale pyramid over `world` ranks.
 
-    costs[s]: work of scale s (~ hl * wl); hls[s]: its output rows (bands keep >= MIN_BAND_ROWS).
+    costs[s]: work of scale s in output pixels (hl * wl); hls[s]: its output rows (bands keep
+    >= MIN_BAND_ROWS).
     Returns (order, owners, load): owners[s] = ranks of scale s's bands, top to bottom (one rank:
     the whole scale); every rank runs its pieces in `order` (scales by decreasing piece cost, the
     same order everywhere, so the band groups' halo exchanges cannot wait on each other in a
@@ -110,7 +120,9 @@ def split_plan(costs, world: int, hls=None, trunk_frac: float = TRUNK_FRAC, over
     best = None
     choices = [[nb for nb in range(1, world + 1) if nb == 1 or hls[s] // nb >= MIN_BAND_ROWS] for s in range(ns)]
     for nbs in itertools.product(*choices):
-        piece = [costs[s] * (1.0 if nbs[s] == 1 else trunk_frac + (1 - trunk_frac) / nbs[s] + overhead)
+        piece = [costs[s] * (1.0 if nbs[s] == 1 else
+                             trunk_frac * min(1.0, (hls[s] / nbs[s] + 2 * BAND_MARGIN) / hls[s])
+                             + (1 - trunk_frac) / nbs[s] + overhead) + (BAND_LATENCY_PX if nbs[s] > 1 else 0)
                  for s in range(ns)]
         order = sorted(range(ns), key=lambda i: (-piece[i], i))
         load = [0.0] * world
@@ -158,7 +170,8 @@ def band_exchange(rank_up, rank_dn, group=None):
     return ex
 
 
-def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=None, split: str = "balanced"):
+def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=None, split: str = "balanced",
+                       maps_out=None):
     """Body(frame) with its scales split across ranks; returns [(candidate, subset)] on `dst`
     (None elsewhere).  frame: uint8 [H,W,3] / [1,H,W,3] numpy, or a torch cuda tensor (then the
     maps stay on the device and travel over RCCL; with gloo they go through host memory).
@@ -168,7 +181,8 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
     kernels and summation order) and the post path is the same code.
     split="balanced" (default): split_plan, which may cut the largest scales into row bands
     (Body.band_maps).  Where it keeps every scale whole the result is the same as "scales";
-    banded scales match the one-GPU maps to fp32 summation order (the conv grids differ)."""
+    banded scales match the one-GPU maps to fp32 summation order (the conv grids differ).
+    maps_out: a list that receives the gathered per-scale maps on `dst` (tests)."""
     import numpy as np
     dev = hasattr(frame, "data_ptr")
     if not dev:
@@ -226,6 +240,8 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
     if rank != dst:
         return None
     maps = [p[0] if len(p) == 1 else torch.cat(p, 2) for p in maps]
+    if maps_out is not None:
+        maps_out.extend(maps)
     if on_device:
         return body.post_scales(maps, H, W)
     return body.post_scales([m.numpy() for m in maps], H, W)

@@ -187,11 +187,11 @@ def test_scale_plan_balances_largest_first():
 def test_split_plan_cuts_the_largest_scale_into_bands():
     """split_plan (src/dist.py): C5's pyramid (hl x wl = 23x41, 46x82, 69x123, 92x164 at 1080p)
     over 1 / 2 / 4 / 8 ranks.  Two ranks keep whole scales (then the result stays bit-identical
-    to one GPU); four and eight cut the 2.0 scale (and at eight the 1.5 scale) into row bands,
-    lowering the modelled critical path below the whole 2.0 scale (the longest-first bound)."""
+    to one GPU); four and eight cut the 2.0 scale (and smaller ones) into row bands, lowering the
+    modelled critical path well below the whole 2.0 scale (the longest-first bound)."""
     import sys
     sys.path.insert(0, PKG)
-    from src.dist import band_rows, split_plan, TRUNK_FRAC
+    from src.dist import band_rows, split_plan
     geo = [(23, 41), (46, 82), (69, 123), (92, 164)]
     costs = [h * w for h, w in geo]
     hls = [h for h, _ in geo]
@@ -200,10 +200,10 @@ def test_split_plan_cuts_the_largest_scale_into_bands():
     _, owners, load = split_plan(costs, 2, hls)
     assert all(len(o) == 1 for o in owners) and max(load) == costs[3]
     _, owners, load = split_plan(costs, 4, hls)
-    assert len(owners[3]) == 2 and max(load) < 0.75 * costs[3]
+    assert len(owners[3]) >= 2 and max(load) < 0.8 * costs[3]
     _, owners, load = split_plan(costs, 8, hls)
-    assert len(owners[3]) >= 4 and max(load) < 0.55 * costs[3]
-    assert max(load) > TRUNK_FRAC * costs[3]          # the replicated trunk bounds it
+    assert len(owners[3]) >= 4 and max(load) < 0.5 * costs[3]
+    assert max(load) > sum(costs) / 8                 # never better than a perfect split
     for w in (3, 4, 5, 8):
         order, owners, load = split_plan(costs, w, hls)
         for s, rs in enumerate(owners):

@@ -1,15 +1,21 @@
 """GPU: row bands of one scale (opose_body_band_maps) — the balanced C5 split (SURVEY.md §8(e):
 "balance them, because 736x1312 is 53 % of FLOPs").
 
-A band rank runs the trunk on the whole scale and the CPM stages (src/model.py:106-133) on its
-own output rows, with 3 halo rows exchanged before every 3x3 / 7x7 stage layer.
+A band rank runs the trunk on its rows plus a 10-row margin past each cut (recomputed) and the
+CPM stages (src/model.py:106-133) on its own output rows, with 3 halo rows exchanged before
+every 3x3 / 7x7 stage layer.
 
 * exact bands (OPOSE_BAND_DP: whole data-parallel tiles, one summation order per pixel) put
   together equal the single whole-height band bit for bit — the halo exchange is lossless;
 * default bands (stream-K grids per band) equal opose_body_scale_maps within the network
   tolerance of tests/test_gpu_parity.py (fp32 summation order only);
-* body_scale_sharded(split="balanced") with four gloo ranks on cuda:0 (the 2.0 scale cut into two
-  bands) gives Body(frame)'s keypoints and people (north-star bar)."""
+* body_scale_sharded(split="balanced") with four gloo ranks on cuda:0 (the 2.0 scale cut into
+  bands, and smaller scales too): every scale's gathered maps within the network tolerance of
+  Body's, and Body(frame)'s people.  Keypoints: the banded maps differ from the one-GPU maps by
+  ~1e-5 of their range (other conv grids, fp32 summation order), which can move a peak one pixel
+  at a near-tie (1 of 316 on this frame; the maps are bit-identical to the threaded bands of
+  scripts/band_diag.py), so the bar is: every peak within 1 px with its part id, at most 1 % of
+  them moved, unmoved peaks' scores within 1e-3, identical person/subset assignment."""
 import os
 import threading
 
@@ -135,16 +141,31 @@ def _balanced_worker(rank, world, port, q):
         geo = b.scale_geom(*HW)
         _, owners, _ = split_plan([g[0] * g[1] for g in geo], world, [g[0] for g in geo])
         banded = len(owners[3]) > 1
-        out = body_scale_sharded(b, img, rank, world, split="balanced")
+        got_maps = []
+        out = body_scale_sharded(b, img, rank, world, split="balanced", maps_out=got_maps)
         msg = ""
         if rank == 0:
             (cand, subset), = out
             (rc, rs), = b.batch(img[None])
             ok = banded and cand.shape == rc.shape and subset.shape == rs.shape and len(cand) > 0
-            ok = ok and np.array_equal(cand[:, [0, 1, 3]], rc[:, [0, 1, 3]])
-            ok = ok and np.allclose(cand[:, 2], rc[:, 2], rtol=1e-3, atol=1e-4)
-            ok = ok and np.array_equal(subset[:, :18], rs[:, :18]) and np.array_equal(subset[:, 19], rs[:, 19])
-            msg = "banded=%s peaks %d/%d people %d/%d" % (banded, len(cand), len(rc), len(subset), len(rs))
+            for s, m in enumerate(got_maps):  # each scale's gathered maps within the network tolerance
+                ref = b.scale_maps(img, s)
+                err = float(np.abs(np.asarray(m) - ref).max())
+                if err > 2e-4 * float(np.abs(ref).max()):
+                    ok = False
+                    msg += "scale %d owners %s max err %.3g at %s; " % (
+                        s, owners[s], err, np.unravel_index(np.abs(np.asarray(m) - ref).argmax(), ref.shape))
+            msg += "banded=%s peaks %d/%d people %d/%d" % (banded, len(cand), len(rc), len(subset), len(rs))
+            if ok:
+                moved = (cand[:, :2] != rc[:, :2]).any(1)
+                checks = {"id": np.array_equal(cand[:, 3], rc[:, 3]),
+                          "xy_1px": float(np.abs(cand[:, :2] - rc[:, :2]).max()) <= 1.0,
+                          "moved_1pct": moved.sum() <= 0.01 * len(cand),
+                          "score": np.allclose(cand[~moved, 2], rc[~moved, 2], rtol=1e-3, atol=1e-4),
+                          "parts": np.array_equal(subset[:, :18], rs[:, :18]),
+                          "count": np.array_equal(subset[:, 19], rs[:, 19])}
+                ok = all(checks.values())
+                msg += " %s moved %d" % (checks, int(moved.sum()))
         else:
             ok = out is None
         q.put((rank, bool(ok), msg))
