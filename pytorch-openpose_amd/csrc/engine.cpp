@@ -263,9 +263,8 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_CONV12_WIN");
         return !(e && e[0] == '0');
     }();
-    // row-band stages (opose_body_band_maps): 0 off; 1: every 3x3 / 7x7 on the window kernel
-    // (it reads the halo rows the band exchange writes; conv_x6 bounds rows to the band);
-    // 2: the same on whole data-parallel tiles (OPOSE_BAND_DP)
+    // inside opose_body_band_maps: 1 (planner's grids), 2: OPOSE_BAND_DP (every conv on whole
+    // data-parallel tiles: each pixel's sum in one fixed order whatever the band); 0 otherwise
     int band_win = 0;
     DevBuf frames, mids[2][kMaxScales], avg, cnt, list, peak_pos, part_cnt, score, conn, conn_cnt, records, maps_in,
         hlab, hsums, hpeaks, hfound, list_score, hsel;
@@ -273,7 +272,7 @@ struct opose_ctx {
     // network workspace, one set per concurrently running scale (slot s runs on scale_stream(s);
     // slot 0 is the handle's stream): input, activations, stream-K slabs
     struct NetWS {
-        DevBuf x, x6in, x6A, x6B, x6P0, x6P1, x6Q0, x6Q1, x6S0, x6S1, x6T0, x6T1, x6U, bufA, bufB, S0, S1, T0, T1, U, partial;
+        DevBuf x, xband, x6in, x6A, x6B, x6P0, x6P1, x6Q0, x6Q1, x6S0, x6S1, x6T0, x6T1, x6U, bufA, bufB, S0, S1, T0, T1, U, partial;
     };
     NetWS ws[kMaxScales];
     int slot = 0;
@@ -1210,6 +1209,9 @@ struct Band {
 
 // bytes of one direction of a band's halo exchange at wl columns: 3 pieces x 32 groups (the
 // widest stage tensor, 256 channels) x 3 rows x (wl + 3) units x 16 B
+// output rows of a band's trunk past each cut edge (engine body_net_x6; src/dist.py BAND_MARGIN)
+constexpr int kBandTrunkMargin = 10;
+
 static size_t band_halo_bytes(int wl) { return (size_t)3 * 32 * 3 * (wl + 3) * 16; }
 
 // bodypose_model.forward on X6 activations, every segment in lockstep; per segment the fp32
@@ -1296,13 +1298,26 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
         run_conv_x6_segs(h, cs);
     };
     auto none = [](size_t) { return XAct{}; };
-    run_trunk_x6(h, net, segs, last, dup);
-    // from here on, a band's convs read halo rows: window kernel only (opose_ctx::band_win)
-    struct BandWin {
-        opose_ctx* h;
-        ~BandWin() { h->band_win = 0; }
-    } band_win_reset{h};
-    if (band) h->band_win = h->band_win ? h->band_win : 1;
+    if (band) {
+        // the band's trunk on the input rows its stages need: out1 rows [r0 - 3, r1 + 3) (the 7x7
+        // Mconv1 halo) plus kBandTrunkMargin - 3 rows that a cut edge's zero padding corrupts
+        // (1 + 1 rows at H, 2 at H/2, 4 at H/4, 4 at H/8: 6.75 rows at H/8); rows a multiple of 8
+        // so the three pools see the whole frame's 2x2 windows
+        const int hl = bs[0].hl, Wp = segs[0].Wp, Hp = segs[0].Hp;
+        const int a = std::max(0, band->r0 - kBandTrunkMargin), b = std::min(hl, band->r1 + kBandTrunkMargin);
+        const int Hs = 8 * (b - a);
+        float* xs = h->ws[segs[0].slot].xband.ensure<float>((size_t)3 * Hs * Wp, h->stream);
+        OPOSE_HIP_CHECK(hipMemcpy2DAsync(xs, (size_t)Hs * Wp * 4, segs[0].x + (size_t)8 * a * Wp, (size_t)Hp * Wp * 4,
+                                         (size_t)Hs * Wp * 4, 3, hipMemcpyDeviceToDevice, h->stream));
+        auto sub = [&](XAct v) {
+            v.l.o0 += (uint32_t)a * v.l.rs;
+            v.l.fs = (uint32_t)(b - a + 3) * v.l.rs;
+            return v;
+        };
+        run_trunk_x6(h, net, {NetSeg{xs, 1, Hs, Wp, segs[0].slot}}, {sub(last[0])}, {sub(dup[0])});
+    } else {
+        run_trunk_x6(h, net, segs, last, dup);
+    }
     layer("conv5_1_CPM_L1+L2", "", [&](size_t i) { return s_(i, 0, 8); }, [&](size_t i) { return t_(i, 0, 0); }, none,
           none, true, false);
     band_halo(bs[0].T[0], TG, 0, TG);
@@ -2319,6 +2334,10 @@ int opose_body_band_maps(opose_t* h, const uint8_t* bgr, int H, int W, int64_t r
                           (float)p.pad_value / 256.f - 0.5f, x, h->stream);
         const size_t cap = xbuf_bytes / 4;
         const Band band{r0, r1, out, fn, user, static_cast<uint8_t*>(xbuf), cap};
+        struct BandWin {  // the band's grid policy for this call only, also when it throws
+            opose_ctx* h;
+            ~BandWin() { h->band_win = 0; }
+        } band_win_reset{h};
         h->band_win = (flags & OPOSE_BAND_DP) ? 2 : 1;
         body_net_x6(h, {NetSeg{x, 1, g.Hp, g.Wp, h->slot}}, &band);
         if (!(flags & OPOSE_OUT_DEVICE)) {

@@ -160,14 +160,17 @@ class Body(object):
             ptr, rs = frame.ctypes.data, frame.strides[0]
         hl, wl, _, _ = self.scale_geom(H, W)[s]
         cap = int(_native.lib.opose_body_band_halo_bytes(wl))
-        xbuf = torch.empty(4 * cap, dtype=torch.uint8, device=torch.device("cuda", self.handle.device))
+        xbuf = getattr(self, "_band_xbuf", None)  # kept across calls (27 exchanges per call)
+        if xbuf is None or xbuf.numel() < 4 * cap:
+            xbuf = self._band_xbuf = torch.empty(4 * cap, dtype=torch.uint8,
+                                                 device=torch.device("cuda", self.handle.device))
         err = []
 
         def _cb(user, nbytes, stream):
             try:
                 if exchange is None:
                     raise RuntimeError("row band with neighbours but no exchange")
-                exchange(xbuf, cap, int(nbytes), stream)
+                exchange(xbuf[:4 * cap], cap, int(nbytes), stream)
                 return 0
             except BaseException as e:  # reported after the call returns
                 err.append(e)
@@ -179,7 +182,7 @@ class Body(object):
             out = torch.empty((1, 57, r1 - r0, wl), dtype=torch.float32, device=frame.device)
             self.handle.wait_torch()
             rc = _native.lib.opose_body_band_maps(self.handle.h, ptr, H, W, rs, self.params, s, r0, r1,
-                                                  out.data_ptr(), cb, None, xbuf.data_ptr(), xbuf.numel(),
+                                                  out.data_ptr(), cb, None, xbuf.data_ptr(), 4 * cap,
                                                   flags | _native.IN_DEVICE | _native.OUT_DEVICE)
             if err:
                 raise err[0]
@@ -189,7 +192,7 @@ class Body(object):
         self.handle.wait_torch()  # xbuf was allocated on torch's stream
         out = np.empty((1, 57, r1 - r0, wl), np.float32)
         rc = _native.lib.opose_body_band_maps(self.handle.h, ptr, H, W, rs, self.params, s, r0, r1, out.ctypes.data,
-                                              cb, None, xbuf.data_ptr(), xbuf.numel(), flags)
+                                              cb, None, xbuf.data_ptr(), 4 * cap, flags)
         if err:
             raise err[0]
         self.handle.check(rc)
