@@ -107,6 +107,18 @@ def pmc_traffic():
     return num / den if den else None
 
 
+def pmc_traffic_lib_match():
+    """True when profiles/pmc_summary.json was collected from the libopose.so this run loads
+    (scripts/pmc_summary.py records its md5), False when it is stale, None without a record."""
+    import hashlib
+    try:
+        meta = json.load(open(os.path.join(REPO, "profiles", "pmc_summary.json"))).get("_meta", {})
+        lib = os.environ.get("OPOSE_LIB") or os.path.join(REPO, "pytorch-openpose_amd", "lib", "libopose.so")
+        return meta["libopose_md5"] == hashlib.md5(open(lib, "rb").read()).hexdigest()
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 # per-stage roofline (north_star: "achieved fraction of MFMA/HBM roofline reported per stage"):
 # conv classes against the fp32 matrix peak; streaming kernels against HBM with the algorithmic
 # bytes the engine records per launch (csrc/engine.cpp prof_begin); the pair-scoring, matching
@@ -476,7 +488,8 @@ def main():
                                         "multiply-add (algorithmic fp32 FLOPs)") if X6 else "fp32 MFMA peak",
                          "per_launch_flops": c7["flops"] / max(1, c7["count"]),
                          "mean_launch_ms": c7["ms"] / max(1, c7["count"]), "traffic": pmc_traffic(),
-                         "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE)*1KiB, profiles/pmc_summary.json"},
+                         "traffic_unit": "bytes per launch (FETCH_SIZE*2 + WRITE_SIZE)*1KiB, profiles/pmc_summary.json",
+                         "traffic_same_library": pmc_traffic_lib_match()},
             "network_tflops": net_flops / (net_ms * 1e-3) / 1e12 if net_ms > 0 else 0.0,
             "stage_breakdown": f"separate profiled pass of {prof_steps} steps after the timed region "
                                "(events around every launch); the timed region brackets only the 7x7 convs",

@@ -48,4 +48,11 @@ for k, d in sorted(agg.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[
     for c, v in sorted(rec.items()):
         print(f"   {c:28s} {v:18.6g}")
 if args.json:
+    # provenance: the library these counters were collected from (bench.py compares it with the
+    # library it runs, so a stale summary is reported as such)
+    import hashlib
+    import os
+    lib = os.environ.get("OPOSE_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                      "pytorch-openpose_amd", "lib", "libopose.so")
+    out["_meta"] = {"libopose_md5": hashlib.md5(open(lib, "rb").read()).hexdigest()}
     json.dump(out, open(args.json, "w"), indent=1)
