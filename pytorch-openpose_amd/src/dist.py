@@ -155,11 +155,10 @@ def band_exchange(rank_up, rank_dn, group=None):
             return
         if xbuf.is_cuda:
             torch.cuda.ExternalStream(stream, device=xbuf.device).synchronize()  # send halves packed
-        host = xbuf[:2 * cap].cpu()
         recv = {o: torch.empty(n, dtype=torch.uint8) for _, o in pairs}
         reqs = []
         for r, o in pairs:
-            reqs.append(dist.isend(host[o * cap:o * cap + n].clone(), r, group=group))
+            reqs.append(dist.isend(xbuf[o * cap:o * cap + n].cpu(), r, group=group))
             reqs.append(dist.irecv(recv[o], r, group=group))
         for q in reqs:
             q.wait()
