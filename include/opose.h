@@ -165,7 +165,7 @@ int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, i
  * into xbuf's send halves on its stream, calls fn(user, bytes, stream), and unpacks the recv
  * halves.  fn moves send_up to the band above (its recv_dn) and send_dn to the band below (its
  * recv_up), ordered on `stream` (a hipStream_t) or synchronously, and returns 0; it is called
- * 27 times per frame and never for a single band covering every row.
+ * 27 times per frame and never for a single band covering every row (fn == NULL: see below).
  *   xbuf: device memory, 4 x opose_body_band_halo_bytes(wl) bytes = [send_up | send_dn |
  *         recv_up | recv_dn];  r1 - r0 >= 3;  maps [57, r1-r0, wl] fp32 (host unless
  *         OPOSE_OUT_DEVICE);  bgr one H x W frame (device with OPOSE_IN_DEVICE);
@@ -173,6 +173,12 @@ int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, i
  * Concatenating every band's maps gives opose_body_scale_maps(s) within fp32 summation-order
  * differences (split-bf16 accuracy). */
 typedef int (*opose_halo_fn)(void* user, size_t bytes, void* stream);
+/* fn == NULL: the library exchanges the halos itself, RCCL send/recv on the handle's stream with
+ * the ranks set by opose_set_band_peers, over the communicator of opose_rccl_init (no host code
+ * between the stage layers). */
+int opose_rccl_unique_id(void* id, size_t len);  /* len >= 128; call on one rank, share the bytes */
+int opose_rccl_init(opose_t* h, const void* id, int rank, int nranks);
+int opose_set_band_peers(opose_t* h, int up, int dn);  /* communicator ranks; -1: none */
 size_t opose_body_band_halo_bytes(int wl);
 int opose_body_band_maps(opose_t* h, const uint8_t* bgr, int H, int W, int64_t row_stride,
                          const opose_params* p, int s, int r0, int r1, float* maps,

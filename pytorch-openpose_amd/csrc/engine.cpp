@@ -7,7 +7,9 @@
 // The network runs as ~60 launches of the implicit-GEMM conv kernel (conv.hip); the two
 // CPM branches of a stage share one launch (combined M for their common first conv,
 // two GEMM groups for the rest); stage concatenation is implicit (channel-slice writes).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -367,7 +369,12 @@ struct opose_ctx {
         }
         pending.erase(pending.begin(), pending.begin() + done);
     }
-    ~opose_ctx() {
+    // RCCL communicator for row-band halo exchanges (opose_rccl_init) and this handle's band
+    // neighbours (opose_set_band_peers; -1: none)
+    ncclComm_t comm = nullptr;
+    int band_up = -1, band_dn = -1;
+    ~opose_ctx();
+    void release() {
         if (nstream) {
             (void)hipStreamSynchronize(nstream);
             (void)hipStreamDestroy(nstream);
@@ -501,6 +508,55 @@ TileChoice choose_win(int Mpad, const std::vector<int>& gpix, int nK, double eff
 }  // namespace
 
 // ======================================================================== engine
+namespace opose {
+
+// RCCL entry points, resolved on first use: the library shares the RCCL a host framework already
+// loaded (torch's), and callers that never split a frame never load it.
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+static const Rccl& rccl() {
+    static const Rccl r = [] {
+        void* lib = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+        if (!lib) lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!lib) lib = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (!lib) throw std::runtime_error("RCCL (librccl.so) not found");
+        auto sym = [&](const char* n) {
+            void* f = dlsym(lib, n);
+            if (!f) throw std::runtime_error(std::string("RCCL without ") + n);
+            return f;
+        };
+        Rccl x;
+        x.get_unique_id = reinterpret_cast<decltype(x.get_unique_id)>(sym("ncclGetUniqueId"));
+        x.comm_init_rank = reinterpret_cast<decltype(x.comm_init_rank)>(sym("ncclCommInitRank"));
+        x.comm_destroy = reinterpret_cast<decltype(x.comm_destroy)>(sym("ncclCommDestroy"));
+        x.send = reinterpret_cast<decltype(x.send)>(sym("ncclSend"));
+        x.recv = reinterpret_cast<decltype(x.recv)>(sym("ncclRecv"));
+        x.group_start = reinterpret_cast<decltype(x.group_start)>(sym("ncclGroupStart"));
+        x.group_end = reinterpret_cast<decltype(x.group_end)>(sym("ncclGroupEnd"));
+        x.error_string = reinterpret_cast<decltype(x.error_string)>(sym("ncclGetErrorString"));
+        return x;
+    }();
+    return r;
+}
+static void rccl_check(ncclResult_t r) {
+    if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL: ") + rccl().error_string(r));
+}
+
+}  // namespace opose
+
+opose_ctx::~opose_ctx() {
+    if (comm) (void)opose::rccl().comm_destroy(comm);
+    release();
+}
+
 namespace opose {
 
 static DevConv* find_conv(opose_ctx* h, int net, const std::string& name) {
@@ -1279,7 +1335,21 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
         ProfEntry pe;
         h->prof_begin(pe, "band_halo", 0, 4.0 * (double)bytes);
         launch_x6p_halo(buf, ps, (uint32_t)plane, g0, ng, P, 3 + band->r0, band->r1, x, x + c, mask, false, h->stream);
-        if (band->fn(band->user, bytes, h->stream) != 0) throw std::runtime_error("row band: halo exchange failed");
+        if (!band->fn) {  // the library's own exchange: RCCL P2P on the handle's stream
+            const Rccl& R = rccl();
+            rccl_check(R.group_start());
+            if (mask & 1) {
+                rccl_check(R.send(x, bytes, ncclUint8, h->band_up, h->comm, h->stream));
+                rccl_check(R.recv(x + 2 * c, bytes, ncclUint8, h->band_up, h->comm, h->stream));
+            }
+            if (mask & 2) {
+                rccl_check(R.send(x + c, bytes, ncclUint8, h->band_dn, h->comm, h->stream));
+                rccl_check(R.recv(x + 3 * c, bytes, ncclUint8, h->band_dn, h->comm, h->stream));
+            }
+            rccl_check(R.group_end());
+        } else if (band->fn(band->user, bytes, h->stream) != 0) {
+            throw std::runtime_error("row band: halo exchange failed");
+        }
         launch_x6p_halo(buf, ps, (uint32_t)plane, g0, ng, P, band->r0, 3 + band->r1, x + 2 * c, x + 3 * c, mask, true,
                         h->stream);
         h->prof_end(pe);
@@ -2305,18 +2375,54 @@ int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, i
     });
 }
 
+int opose_rccl_unique_id(void* id, size_t len) {
+    if (!id || len < sizeof(ncclUniqueId)) return OPOSE_E_ARG;
+    try {
+        ncclUniqueId u;
+        rccl_check(rccl().get_unique_id(&u));
+        std::memcpy(id, &u, sizeof(u));
+        return OPOSE_OK;
+    } catch (const std::exception&) {
+        return OPOSE_E_HIP;
+    }
+}
+
+int opose_rccl_init(opose_t* h, const void* id, int rank, int nranks) {
+    if (!h || !id || nranks < 1 || rank < 0 || rank >= nranks) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        if (h->comm) {
+            rccl_check(rccl().comm_destroy(h->comm));
+            h->comm = nullptr;
+        }
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        rccl_check(rccl().comm_init_rank(&h->comm, nranks, u, rank));
+        return OPOSE_OK;
+    });
+}
+
+int opose_set_band_peers(opose_t* h, int up, int dn) {
+    if (!h) return OPOSE_E_ARG;
+    h->band_up = up;
+    h->band_dn = dn;
+    return OPOSE_OK;
+}
+
 size_t opose_body_band_halo_bytes(int wl) { return wl > 0 ? band_halo_bytes(wl) : 0; }
 
 int opose_body_band_maps(opose_t* h, const uint8_t* bgr, int H, int W, int64_t row_stride, const opose_params* pp,
                          int s, int r0, int r1, float* maps, opose_halo_fn fn, void* user, void* xbuf,
                          size_t xbuf_bytes, int flags) {
-    if (!h || !bgr || !maps || !fn || !xbuf || H <= 0 || W <= 0 || row_stride < (int64_t)W * 3) return OPOSE_E_ARG;
+    if (!h || !bgr || !maps || !xbuf || H <= 0 || W <= 0 || row_stride < (int64_t)W * 3) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
         enter_main(h);
         const opose_params p = fill_params(pp, OPOSE_NET_BODY);
         if (s < 0 || s >= p.n_scales) return OPOSE_E_ARG;
         const ScaleGeom g = geom(p.scales[s], p, H, W);
         if (r0 < 0 || r1 > g.hl || r1 - r0 < 3) return OPOSE_E_ARG;
+        if (!fn && ((r0 > 0 && (!h->comm || h->band_up < 0)) || (r1 < g.hl && (!h->comm || h->band_dn < 0))))
+            return OPOSE_E_ARG;  // the library's exchange needs opose_rccl_init + opose_set_band_peers
         if (xbuf_bytes < 4 * band_halo_bytes(g.wl)) return OPOSE_E_ARG;
         if (!h->x6) throw std::invalid_argument("row bands need the split-bf16 path (OPOSE_CONV=f32 is set)");
         if (!h->loaded[OPOSE_NET_BODY]) throw std::runtime_error("body weights not loaded");

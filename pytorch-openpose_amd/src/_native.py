@@ -58,6 +58,9 @@ def _load():
         "opose_body_scale_maps": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), I, P, I]),
         "opose_body_post_scales": (I, [P, C.POINTER(P), P, P, P, P, I, I, I, I, C.POINTER(Params), P, I]),
         "opose_body_band_halo_bytes": (S, [I]),
+        "opose_rccl_unique_id": (I, [P, S]),
+        "opose_rccl_init": (I, [P, P, I, I]),
+        "opose_set_band_peers": (I, [P, I, I]),
         "opose_body_band_maps": (I, [P, P, I, I, C.c_int64, C.POINTER(Params), I, I, I, P, HALO_FN, P, P, S, I]),
         "opose_hand_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, P, I]),
         "opose_hand_post": (I, [P, C.POINTER(P), P, P, P, P, I, I, I, I, C.POINTER(Params), P, P, I]),
@@ -95,7 +98,7 @@ EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last
             "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_hand_forward_pyramid",
             "opose_body_infer",
             "opose_body_post", "opose_body_scale_geom", "opose_body_scale_maps",
-            "opose_body_post_scales", "opose_body_band_halo_bytes", "opose_body_band_maps", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
+            "opose_body_post_scales", "opose_body_band_halo_bytes", "opose_body_band_maps", "opose_rccl_unique_id", "opose_rccl_init", "opose_set_band_peers", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
             "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_conv_time", "opose_debug_conv_x6", "opose_debug_conv_x6_time", "opose_debug_preprocess",
             "opose_debug_heat", "opose_debug_hand_label"]
 
@@ -186,6 +189,22 @@ class Handle:
 
     def synchronize(self):
         self.check(lib.opose_synchronize(self.h))
+
+    # ---- RCCL for row-band halo exchanges (opose_body_band_maps with the library's exchange)
+    @staticmethod
+    def rccl_unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        rc = lib.opose_rccl_unique_id(buf, 128)
+        if rc != OPOSE_OK:
+            raise OposeError(rc, "ncclGetUniqueId failed")
+        return bytes(buf)
+
+    def rccl_init(self, uid: bytes, rank: int, nranks: int):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid[:128])
+        self.check(lib.opose_rccl_init(self.h, buf, int(rank), int(nranks)))
+
+    def set_band_peers(self, up, dn):
+        self.check(lib.opose_set_band_peers(self.h, -1 if up is None else int(up), -1 if dn is None else int(dn)))
 
     # ---- ordering against torch's current stream (every device-tensor entry point)
     def _adopt_torch_stream(self):

@@ -145,7 +145,9 @@ class Body(object):
         between neighbouring bands (src.dist.band_exchange): xbuf is the uint8 device tensor
         [send_up | send_dn | recv_up | recv_dn] of `cap` bytes each, `stream` the library's
         hipStream_t, on which the send halves are being packed.  Not needed when one band covers
-        every row.  exact: whole data-parallel tiles (bit-identical to any other banding)."""
+        every row.  exchange="rccl": the library's own RCCL send/recv on its stream, with the
+        communicator and neighbours of src.dist.init_band_comm / Handle.set_band_peers (no Python
+        between the layers).  exact: whole data-parallel tiles (bit-identical to any banding)."""
         import torch
         dev = hasattr(frame, "data_ptr")
         if dev:
@@ -176,7 +178,7 @@ class Body(object):
                 err.append(e)
                 return 1
 
-        cb = _native.HALO_FN(_cb)
+        cb = _native.HALO_FN() if exchange == "rccl" else _native.HALO_FN(_cb)  # NULL: the library's RCCL
         flags = _native.BAND_DP if exact else 0
         if dev:
             out = torch.empty((1, 57, r1 - r0, wl), dtype=torch.float32, device=frame.device)

@@ -169,6 +169,19 @@ def band_exchange(rank_up, rank_dn, group=None):
     return ex
 
 
+def init_band_comm(body, group=None):
+    """The library's own RCCL communicator over the ranks of `group` (Body.band_maps with
+    exchange="rccl": halo send/recv on the library's stream, no Python between the layers).
+    Rank 0 makes the id; it travels by one broadcast on the group.  Once per Body."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    if getattr(body, "_band_comm", None) == (rank, world):
+        return
+    obj = [body.handle.rccl_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    body.handle.rccl_init(obj[0], rank, world)
+    body._band_comm = (rank, world)
+
+
 def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=None, split: str = "balanced",
                        maps_out=None):
     """Body(frame) with its scales split across ranks; returns [(candidate, subset)] on `dst`
@@ -214,7 +227,12 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
             r0, r1 = band_rows(geoms[s][0], len(owners[s]))[b]
             up = owners[s][b - 1] if b > 0 else None
             dn = owners[s][b + 1] if b + 1 < len(owners[s]) else None
-            m = body.band_maps(local[0], s, r0, r1, band_exchange(up, dn, group))
+            if on_device:  # RCCL: the library exchanges the halos itself
+                init_band_comm(body, group)
+                body.handle.set_band_peers(up, dn)
+                m = body.band_maps(local[0], s, r0, r1, "rccl")
+            else:
+                m = body.band_maps(local[0], s, r0, r1, band_exchange(up, dn, group))
         pieces[(s, owners[s].index(rank))] = m if on_device else torch.from_numpy(m)
     maps = [None] * len(geoms)
     reqs = []

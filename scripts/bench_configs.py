@@ -196,13 +196,13 @@ def main():
         load = [sum(t for t, r in zip(net_ms, own) if r == k) for k in range(world)]
         out["C5_sharded_w%d_model_ms_excl_gather" % world] = max(load) + post_ms
     # balanced split (src.dist.split_plan): the largest scales cut into row bands.  A band's time
-    # is measured here with the halo exchange stubbed out (the 27 pack / unpack launches per band
-    # run, the transfer does not); the transfer is modelled as 27 x (10 us + 2 x the halo bytes at
-    # 100 GB/s), the halo bytes being 3 rows x 256 channels x 6 B x (wl + 3) per direction.
+    # is measured here with the library's own RCCL exchange on a one-rank communicator whose
+    # neighbours are the rank itself (the 27 pack / send / recv / unpack steps per band run as on
+    # a node; the bytes move within the GPU); the xGMI transfer is added as 27 x (10 us + 2 x the
+    # halo bytes at 100 GB/s), the halo bytes being 3 rows x 256 channels x 6 B x (wl + 3).
     from src.dist import band_rows, split_plan
-
-    def noop(xbuf, cap, n, stream):
-        return None
+    body5.handle.rccl_init(body5.handle.rccl_unique_id(), 0, 1)
+    body5.handle.set_band_peers(0, 0)
     costs, hls = [g[0] * g[1] for g in geoms], [g[0] for g in geoms]
     band_ms = {}
     for world in (2, 4, 8):
@@ -216,7 +216,7 @@ def main():
                 if (s, nb) not in band_ms:
                     xfer = 27 * (10e-3 + 2 * 3 * 256 * 6 * (geoms[s][1] + 3) / 100e9 * 1e3)
                     band_ms[(s, nb)] = max(
-                        timed(lambda r=r: body5.band_maps(f1, s, r[0], r[1], noop), 5, warm=1)
+                        timed(lambda r=r: body5.band_maps(f1, s, r[0], r[1], "rccl"), 5, warm=1)
                         for r in band_rows(geoms[s][0], nb)) + xfer
                 t = band_ms[(s, nb)]
             for r in owners[s]:
