@@ -172,7 +172,8 @@ def band_exchange(rank_up, rank_dn, group=None):
 def init_band_comm(body, group=None):
     """The library's own RCCL communicator over the ranks of `group` (Body.band_maps with
     exchange="rccl": halo send/recv on the library's stream, no Python between the layers).
-    Rank 0 makes the id; it travels by one broadcast on the group.  Once per Body."""
+    Rank 0 makes the id; it travels by one broadcast on the group.  Collective: every rank of
+    the group calls it (once per Body; later calls return at once)."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     if getattr(body, "_band_comm", None) == (rank, world):
         return
@@ -216,6 +217,8 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
         raise ValueError("split must be 'balanced' or 'scales'")
     on_device = dev and dist.get_backend(group) == "nccl"
     local = frame if on_device else (frame.cpu().numpy() if dev else frame)
+    if on_device and any(len(o) > 1 for o in owners):
+        init_band_comm(body, group)  # collective: every rank, banded pieces or not
     pieces = {}  # (s, band) -> maps of this rank
     for s in order:
         if rank not in owners[s]:
@@ -228,7 +231,6 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
             up = owners[s][b - 1] if b > 0 else None
             dn = owners[s][b + 1] if b + 1 < len(owners[s]) else None
             if on_device:  # RCCL: the library exchanges the halos itself
-                init_band_comm(body, group)
                 body.handle.set_band_peers(up, dn)
                 m = body.band_maps(local[0], s, r0, r1, "rccl")
             else:

@@ -212,3 +212,86 @@ def test_split_plan_cuts_the_largest_scale_into_bands():
                 assert min(b - a for a, b in band_rows(hls[s], len(rs))) >= 8
     rows = band_rows(92, 5)
     assert rows[0][0] == 0 and rows[-1][1] == 92 and all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
+
+
+class _FakeHandle:
+    def __init__(self):
+        self.inits, self.peers = [], None
+
+    @staticmethod
+    def rccl_unique_id():
+        return bytes(range(128))
+
+    def rccl_init(self, uid, rank, world):
+        self.inits.append((uid, rank, world))
+
+    def set_band_peers(self, up, dn):
+        self.peers = (up, dn)
+
+
+class _FakeRcclBody(_FakeBody):
+    """The device (RCCL) branch of body_scale_sharded: maps as tensors, bands through the
+    library's own exchange (exchange == "rccl" with the peers set on the handle)."""
+
+    def __init__(self):
+        super().__init__()
+        self.handle = _FakeHandle()
+
+    def scale_maps(self, frame, s):
+        return torch.from_numpy(super().scale_maps(frame, s))
+
+    def band_maps(self, frame, s, r0, r1, exchange=None, exact=False):
+        assert exchange == "rccl" and len(self.handle.inits) == 1
+        self.bands.append((s, r0, r1, self.handle.peers))
+        return torch.from_numpy(_FakeBody.scale_maps(self, frame[None], s)[:, :, r0:r1].copy())
+
+    def post_scales(self, maps, H, W):
+        return [m.numpy() for m in maps]
+
+
+def _rccl_worker(rank, world, port, q):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from src import dist as sdist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sdist.dist.get_backend = lambda group=None: "nccl"  # exercise the RCCL branch over gloo
+        body = _FakeRcclBody()
+        frame = torch.zeros((90, 160, 3), dtype=torch.uint8)
+        out = sdist.body_scale_sharded(body, frame, rank, world, dst=0, split="balanced")
+        order, owners, _ = sdist.split_plan([g[0] * g[1] for g in GEOMS], world, [g[0] for g in GEOMS])
+        ok = body.handle.inits == [(bytes(range(128)), rank, world)]  # every rank, once
+        want = []
+        for s in order:
+            rs = owners[s]
+            if rank in rs and len(rs) > 1:
+                b = rs.index(rank)
+                want.append((s, *sdist.band_rows(GEOMS[s][0], len(rs))[b],
+                             (rs[b - 1] if b else None, rs[b + 1] if b + 1 < len(rs) else None)))
+        ok &= body.bands == want
+        if rank == 0:
+            for s, m in enumerate(out):
+                ok &= np.array_equal(m, _FakeBody().scale_maps(np.zeros((1, 90, 160, 3), np.uint8), s))
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_balanced_split_rccl_branch_four_ranks():
+    """body_scale_sharded's device branch (RCCL on a node) with four ranks: the library's
+    communicator is set up collectively on every rank (also those without a band), each band
+    rank sets its neighbours before its band, and rank 0 reassembles every scale."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29950 + os.getpid() % 40
+    procs = [ctx.Process(target=_rccl_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(4)}
