@@ -1257,17 +1257,17 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
 struct Band {
     int r0, r1;
     float* maps;  // [57][r1 - r0][wl] fp32 device
-    opose_halo_fn fn;
+    opose_halo_fn fn;  // nullptr: the library's RCCL send / recv (opose_rccl_init)
     void* user;
     uint8_t* xbuf;  // [send_up | send_dn | recv_up | recv_dn], cap bytes each
     size_t cap;
 };
 
-// bytes of one direction of a band's halo exchange at wl columns: 3 pieces x 32 groups (the
-// widest stage tensor, 256 channels) x 3 rows x (wl + 3) units x 16 B
 // output rows of a band's trunk past each cut edge (engine body_net_x6; src/dist.py BAND_MARGIN)
 constexpr int kBandTrunkMargin = 10;
 
+// bytes of one direction of a band's halo exchange at wl columns: 3 pieces x 32 groups (the
+// widest stage tensor, 256 channels) x 3 rows x (wl + 3) units x 16 B
 static size_t band_halo_bytes(int wl) { return (size_t)3 * 32 * 3 * (wl + 3) * 16; }
 
 // bodypose_model.forward on X6 activations, every segment in lockstep; per segment the fp32
