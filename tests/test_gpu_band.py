@@ -9,8 +9,8 @@ every 3x3 / 7x7 stage layer.
   together equal the single whole-height band bit for bit — the halo exchange is lossless;
 * default bands (stream-K grids per band) equal opose_body_scale_maps within the network
   tolerance of tests/test_gpu_parity.py (fp32 summation order only);
-* body_scale_sharded(split="balanced") with four gloo ranks on cuda:0 (the 2.0 scale cut into
-  bands, and smaller scales too): every scale's gathered maps within the network tolerance of
+* body_scale_sharded(split="balanced") with four and eight gloo ranks on cuda:0 (the 2.0 scale
+  cut into 2 / 5 bands, the 1.5 scale into 2 at eight): every scale's gathered maps within the network tolerance of
   Body's, and Body(frame)'s people.  Keypoints: the banded maps differ from the one-GPU maps by
   ~1e-5 of their range (other conv grids, fp32 summation order), which can move a peak one pixel
   at a near-tie (1 of 316 on this frame; the maps are bit-identical to the threaded bands of
@@ -173,12 +173,15 @@ def _balanced_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_balanced_split_four_ranks_matches_body():
+@pytest.mark.parametrize("world", [4, 8])
+def test_balanced_split_matches_body(world):
+    """4 ranks: the 2.0 scale in 2 bands; 8 ranks (C5's node): the 2.0 scale in 5 bands of 18-19
+    rows (middle bands exchange with both neighbours) and the 1.5 scale in 2."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + os.getpid() % 300
-    procs = [ctx.Process(target=_balanced_worker, args=(r, 4, port, q)) for r in range(4)]
+    port = 29500 + world * 37 + os.getpid() % 300
+    procs = [ctx.Process(target=_balanced_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
