@@ -16,6 +16,8 @@
  *   Body.__call__ after the net    src/body.py:52-212        opose_body_post   (parity entry point)
  *   Hand.__call__                  src/hand.py:25-75         opose_hand_infer
  *   Hand.__call__ after the net    src/hand.py:51-75         opose_hand_post   (parity entry point)
+ *   one scale of Body.__call__     src/body.py:36-50         opose_body_scale_maps; its output rows
+ *                                                            opose_body_band_maps (C5 split)
  *
  * Conventions: plain pointers and sizes only; 0 = OK, negative = error (see opose_status).
  * Host pointers are caller-owned and read-only; the library copies them. A handle owns one
