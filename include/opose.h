@@ -62,9 +62,6 @@ enum {
                                 stream and overlaps the previous call's post-network
                                 part; records are still complete in the handle's stream
                                 order. Video-batch throughput mode.                 */
-    OPOSE_BAND_DP = 8,       /* opose_body_band_maps only: every banded conv on whole
-                                data-parallel tiles, so each output pixel sums in one
-                                fixed order whatever the band (bit-identical bands)  */
 };
 
 #define OPOSE_MAX_SCALES 8
@@ -160,9 +157,9 @@ int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, i
 
 /* Row band [r0, r1) of scale s's network maps for ONE frame, for splitting a large scale across
  * ranks (736x1312 is 53 % of the pyramid's FLOPs; src/body.py:36-50 for one
- * m, cut into output rows).  Every rank of a band group runs the VGG trunk on the whole scale
- * (30 % of the scale's FLOPs), then the six CPM stages (src/model.py:106-133) on its own rows
- * only.  Before each 3x3 / 7x7 stage layer that needs them, the 3 rows on either side of the
+ * m, cut into output rows).  Every rank of a band group runs the VGG trunk on its band's rows
+ * plus a 10-row margin past each cut (recomputed, not exchanged), then the six CPM stages
+ * (src/model.py:106-133) on its own rows only.  Before each 3x3 / 7x7 stage layer that needs them, the 3 rows on either side of the
  * band are exchanged with the neighbouring bands: the library packs its top and bottom 3 rows
  * into xbuf's send halves on its stream, calls fn(user, bytes, stream), and unpacks the recv
  * halves.  fn moves send_up to the band above (its recv_dn) and send_dn to the band below (its
@@ -170,16 +167,19 @@ int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, i
  * 27 times per frame and never for a single band covering every row (fn == NULL: see below).
  *   xbuf: device memory, 4 x opose_body_band_halo_bytes(wl) bytes = [send_up | send_dn |
  *         recv_up | recv_dn];  r1 - r0 >= 3;  maps [57, r1-r0, wl] fp32 (host unless
- *         OPOSE_OUT_DEVICE);  bgr one H x W frame (device with OPOSE_IN_DEVICE);
- *   OPOSE_BAND_DP: bit-identical banding (see the flag); default: stream-K grids per band.
- * Concatenating every band's maps gives opose_body_scale_maps(s) within fp32 summation-order
- * differences (split-bf16 accuracy). */
+ *         OPOSE_OUT_DEVICE);  bgr one H x W frame (device with OPOSE_IN_DEVICE).
+ * Every conv sums each pixel in the order the whole frame's network does (k slabs fixed by the
+ * layer and the frame), so concatenating every band's maps gives
+ * opose_body_scale_maps(s) bit for bit. */
 typedef int (*opose_halo_fn)(void* user, size_t bytes, void* stream);
 /* fn == NULL: the library exchanges the halos itself, RCCL send/recv on the handle's stream with
  * the ranks set by opose_set_band_peers, over the communicator of opose_rccl_init (no host code
  * between the stage layers). */
 int opose_rccl_unique_id(void* id, size_t len);  /* len >= 128; call on one rank, share the bytes */
 int opose_rccl_init(opose_t* h, const void* id, int rank, int nranks);
+/* A band rank failed: ncclCommAbort on the handle's communicator (the peers' pending halo
+ * send / recv fail instead of waiting) and drop it; opose_rccl_init builds a new one. */
+int opose_rccl_abort(opose_t* h);
 int opose_set_band_peers(opose_t* h, int up, int dn);  /* communicator ranks; -1: none */
 size_t opose_body_band_halo_bytes(int wl);
 int opose_body_band_maps(opose_t* h, const uint8_t* bgr, int H, int W, int64_t row_stride,

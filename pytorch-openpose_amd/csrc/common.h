@@ -81,7 +81,14 @@ struct X6Group {
     int npix;              // GEMM columns: N*H*W (pooled: N*(H/2)*(W/2)*4, quad-major)
     int ylo, yhi;          // conv_x6 taps read rows [ylo, yhi) (yhi == 0: [0, H)); a row band's
                            // view (engine.cpp Band) also reads its halo rows
+    // k slabs: every tile of this group sums its nK chunks as `slabs` fixed ranges [s nK / slabs,
+    // (s + 1) nK / slabs), each accumulated from zero, folded in slab order by conv_x6_fixup
+    // (slabs == 1: one run over all chunks, written by the conv itself).  The count is a function
+    // of the layer and the segment's logical geometry only (engine.cpp slab_count), never of the
+    // launch's grid, groups or row band: a pixel sums in the same order whatever launch computes it.
+    int slabs;
     int t0;                // first tile of the group in the launch's tile space (set by the launcher)
+    int u0;                // first work unit (tile, slab) of the group (set by the launcher)
 };
 
 // One launch runs up to kX6Groups GEMMs of the same conv shape (ks, Cin, Mpad): the two CPM
@@ -96,9 +103,14 @@ struct X6Args {
     int cin_g;      // channel groups of the conv's input (Cin padded to 8)
     int small;      // 1: one group (Cin <= 8), chunks of 4 taps; 0: chunks of (4 groups, 1 tap)
     int nK;         // chunks of 32 k
-    int Mpad, ngroups, sk_grid;
+    int Mpad, ngroups;
+    int sk_grid;    // workgroups
     int tiles;      // tiles of all groups (set by the launcher)
-    float* partial; // stream-K partial slabs [2 * sk_grid][MT * PT]
+    int units;      // work units (tile, slab) of all groups (set by the launcher)
+    // unit lists: sched[w] .. sched[w + 1] index sched[sk_grid + 1 + i], the units workgroup w runs
+    // (the host's longest-first schedule); nullptr: workgroup w runs units [w U / G, (w + 1) U / G)
+    const int* sched;
+    float* partial; // slab partials [units][MT * PT] (groups with slabs > 1)
     int pool;       // 1: 2x2/2 max-pool fused into the epilogue (npix = N * (H/2) * (W/2) * 4, quad-major)
 };
 

@@ -17,10 +17,12 @@
 //  * Everything else is conv_x6's MODE-2 loop: 128 x 256 tile, 8 waves of 64 x 64, weights by
 //    LDS-DMA into two stages, six piece products per chunk in the order
 //    (0,2) (0,0) (0,1) | barrier | (1,0) (2,0) (1,1), fragments refilled after their last use.
-//  * Data-parallel grids (one workgroup per tile) or stream-K ranges over (tile, chunk) with
-//    conv_x6's partial slabs and fixup; a range may start inside a channel group (its first two
-//    windows are loaded in the prologue).  The host falls back to conv_x6 when a window would
-//    exceed WMAX.
+//  * Work units (tile, k slab): a group's tiles sum their chunks in `slabs` fixed ranges
+//    (common.h X6Group), so the order of every pixel's sum is set by the layer and the segment,
+//    not by the grid; a workgroup runs a list of units (data parallel: one whole tile), a slab
+//    of a multi-slab tile leaves a partial that conv_x6_fixup folds in slab order.  A slab may
+//    start inside a channel group (its first two windows are loaded in the prologue).  The host
+//    falls back to conv_x6 when a window would exceed WMAX.
 //  * The groups of a launch (X6Group: CPM branches, pyramid scales) each carry their own
 //    geometry; a tile's window and pixels come from its group.
 //  * The same kernel runs the batched 3x3 convs on padded inputs (trunk conv3_x / conv4_x and
@@ -60,29 +62,25 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nM = a.Mpad / MT;
-    const int nK = a.nK;
     const int wm0 = (wave % NWM) * WM;
     const int wp0 = (wave / NWM) * WP;
     // two waves per SIMD: the younger half issues first when both are ready (guide T5, static form)
     if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
-    // stream-K range of this workgroup over (tile, chunk), XCD-contiguous (guide T1); a grid of
-    // one workgroup per tile is the data-parallel case.  Pieces run from the range end backwards.
+    // this workgroup's work units (tile, k slab), XCD-contiguous ids (guide T1); a grid of one
+    // workgroup per whole tile is the data-parallel case
     const int Gw = gridDim.x;
     int id;
     {
         const int b = blockIdx.x, q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
         id = xcd * q + min(xcd, rr) + (b >> 3);
     }
-    const long long I = (long long)a.tiles * nK;
-    const long long lo = (long long)id * I / Gw, hi = (long long)(id + 1) * I / Gw;
-    for (long long itp = hi; itp > lo;) {
-    const int tile = (int)((itp - 1) / nK);
-    const int c_end = (int)(itp - (long long)tile * nK);
-    const int c_begin = (int)max<long long>(0, lo - (long long)tile * nK);
-    itp = (long long)tile * nK + c_begin;
-    const int first = itp == lo;
-    const X6Group G = a.g[x6_group_of(a, tile)];
+    const X6Work wk = x6_work_of(a, id);
+    for (int k = wk.k0; k < wk.k1; ++k) {
+    const int uid = wk.list ? wk.list[k] : k;
+    const X6Unit un = x6_unit_of(a, uid);
+    const int tile = un.tile, c_begin = un.c0, c_end = un.c1;
+    const X6Group G = a.g[un.g];
     const int H = G.H, W = G.W, HW = H * W, npix = G.npix;
     const int mt = (tile - G.t0) % nM;
     const int ptl = (tile - G.t0) / nM;
@@ -317,11 +315,11 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the last (unused) reads / loads landed
     fence_all();
 
-    // ---- epilogue: a piece of a shared tile leaves an fp32 partial slab (summed in k order by
+    // ---- epilogue: a slab of a multi-slab tile leaves an fp32 partial (folded in slab order by
     // conv_x6_fixup); a whole tile adds bias + ReLU and writes X6 / X6P slices or fp32 NCHW
-    if (c_begin != 0 || c_end != nK) {
+    if (!un.whole) {
         const __amdgpu_buffer_rsrc_t srs = slab_rsrc(a.partial);
-        const uint32_t sbase = (uint32_t)(2 * id + (first ? 0 : 1)) * (uint32_t)(MT * PT * 4);
+        const uint32_t sbase = (uint32_t)uid * (uint32_t)(MT * PT * 4);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int pl = wp0 + j * 16 + (lane & 15);
@@ -431,6 +429,12 @@ bool conv_win_fits(int N, int H, int W, int ks) {
     return (ks == 3 || ks == 7) && W + 3 <= 1024 && conv_win_units(N, H, W, ks, 256) <= kWinLarge;
 }
 
+bool conv_win_fits_rows(int W, int ks) {
+    // a run starting at column x spans (x + 255) / W + 1 rows: at most (W + 254) / W + 1
+    const int pad = ks / 2, span = (W + 254) / W;
+    return (ks == 3 || ks == 7) && W + 3 <= 1024 && (span + 2 * pad + 1) * (W + 3) + pad <= kWinLarge;
+}
+
 void launch_conv_win_x6(const X6Args& a0, hipStream_t st) {
     if ((a0.ks != 3 && a0.ks != 7) || a0.small || a0.pool || a0.Mpad % 128)
         throw std::invalid_argument("conv_win_x6: unsupported layer");
@@ -442,7 +446,8 @@ void launch_conv_win_x6(const X6Args& a0, hipStream_t st) {
             throw std::invalid_argument("conv_win_x6: input is not X6P");
         need = std::max(need, conv_win_units(G.N, G.H, G.W, a.ks, 256));
     }
-    if (a.sk_grid < 1 || a.sk_grid > a.tiles * a.nK) throw std::invalid_argument("conv_win_x6: bad grid");
+    if (a.sk_grid < 1 || a.sk_grid > a.units) throw std::invalid_argument("conv_win_x6: bad grid");
+    if ((size_t)a.units * 128 * 256 * 4 >= 0x7fffffffull) throw std::invalid_argument("conv_win_x6: too many slabs");
     const dim3 grid(a.sk_grid), blk(512);
     if (need <= kWinSmall) {  // room for a third weight stage (48 + 72 + 24 KB of LDS)
         if (a.ks == 7) hipLaunchKernelGGL((conv_win_x6<128, 256, 7, kWinSmall, kWinStagesSmall>), grid, blk, 0, st, a);
@@ -453,7 +458,7 @@ void launch_conv_win_x6(const X6Args& a0, hipStream_t st) {
     } else {
         throw std::invalid_argument("conv_win_x6: window exceeds LDS");
     }
-    if (a.sk_grid != a.tiles) launch_conv_x6_fixup(a, 128, 256, st);
+    if (a.units != a.tiles) launch_conv_x6_fixup(a, 128, 256, st);
 }
 
 }  // namespace opose

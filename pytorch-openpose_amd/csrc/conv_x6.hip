@@ -65,7 +65,6 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nM = a.Mpad / MT;
-    const int nK = a.nK;
     // geometry of the current tile's group (X6Group N, H, W, npix)
     int H = 0, W = 0, HW = 0, npix = 0, ylo = 0, yspan = 0;
     // pooled conv (a.pool): GEMM columns run over the 2x2 quads of the pooled grid, quad-major
@@ -92,16 +91,13 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
     const int b = blockIdx.x;
     const int q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
     const int id = xcd * q + min(xcd, rr) + (b >> 3);
-    const long long I = (long long)a.tiles * nK;
-    const long long lo = (long long)id * I / Gw, hi = (long long)(id + 1) * I / Gw;
+    const X6Work wk = x6_work_of(a, id);
 
-    for (long long itp = hi; itp > lo;) {
-        const int tile = (int)((itp - 1) / nK);
-        const int c_end = (int)(itp - (long long)tile * nK);
-        const int c_begin = (int)max<long long>(0, lo - (long long)tile * nK);
-        itp = (long long)tile * nK + c_begin;
-        const int first = itp == lo;
-        const X6Group G = a.g[x6_group_of(a, tile)];
+    for (int k = wk.k0; k < wk.k1; ++k) {
+        const int uid = wk.list ? wk.list[k] : k;
+        const X6Unit un = x6_unit_of(a, uid);
+        const int tile = un.tile, c_begin = un.c0, c_end = un.c1;
+        const X6Group G = a.g[un.g];
         H = G.H;
         W = G.W;
         HW = H * W;
@@ -361,7 +357,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
         // accumulator register r of block (i, j): rows (channels) ml0 + (r & 3) of quad r >> 2,
         // column (pixel) pl.  32x32: quad qd covers rows 32i + 8qd + 4hk .. +3, pixel 32j + l31;
         // 16x16: rows 16i + 4(l >> 4) .. +3, pixel 16j + (l & 15).
-        const bool whole = c_begin == 0 && c_end == nK;
+        const bool whole = un.whole;
         const int cout8 = (G.cout + 7) & ~7;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -374,7 +370,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             if (!whole) {
                 static_assert(ACC_N == 4, "slab quads: one 16x16 accumulator block per lane quad");
                 const __amdgpu_buffer_rsrc_t srs = slab_rsrc(a.partial);
-                const uint32_t sbase = (uint32_t)(2 * id + (first ? 0 : 1)) * (uint32_t)(MT * PT * 4);
+                const uint32_t sbase = (uint32_t)uid * (uint32_t)(MT * PT * 4);
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
                     store_slab_quad(srs, sbase + (uint32_t)((quad_row(i, 0) / 4) * PT + pl) * 16u, acc[i][j]);
@@ -466,22 +462,19 @@ __device__ __forceinline__ void store8_x6(uint8_t* unit, uint32_t ps, const floa
     }
 }
 
-// Stream-K fixup: grid (tiles, MT*PT/8/256); each thread finishes one X6 unit (8 channels of one
-// pixel) of a shared tile: partial slabs summed in k order (deterministic).  Pixels run fastest
-// across the lanes, so every slab load is a coalesced 1 KB run of channel quads (x6.h) and every
-// store a whole 16-byte unit; two slabs' loads are in flight per round trip.
+// Slab fixup: grid (tiles, MT*PT/8/256); each thread finishes one X6 unit (8 channels of one
+// pixel) of a multi-slab tile: the slab partials folded in slab order, ((s0 + s1) + s2) + ...
+// (the order is the group's, not the grid's).  Pixels run fastest across the lanes, so every
+// slab load is a coalesced 1 KB run of channel quads (x6.h) and every store a whole 16-byte
+// unit; two slabs' loads are in flight per round trip.
 template <int MT, int PT>
 __global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
     const int nM = a.Mpad / MT;
-    const int nK = a.nK;
-    const long long Gw = a.sk_grid;
-    const long long I = (long long)a.tiles * nK;
     const int tile = blockIdx.x;
-    const long long x0 = (long long)tile * nK;
-    const int w0 = (int)(((x0 + 1) * Gw - 1) / I);
-    const int w1 = (int)(((x0 + nK) * Gw - 1) / I);
-    if (w0 == w1) return;
     const X6Group G = a.g[x6_group_of(a, tile)];
+    const int S = G.slabs;
+    if (S == 1) return;  // written by the conv
+    const int w0 = G.u0 + (tile - G.t0) * S, w1 = w0 + S - 1;  // the tile's slab partials
     const int mt = (tile - G.t0) % nM;
     const int pt = (tile - G.t0) / nM;
     const int HW = G.H * G.W;
@@ -494,9 +487,7 @@ __global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
     if (mg >= (G.out_f32 ? G.cout : cout8)) return;
     // the unit's two channel quads (x6.h slab layout): quads ml0/4 and ml0/4 + 1 of pixel pl
     auto slab = [&](int w) __attribute__((always_inline)) {
-        const long long lo_w = (long long)w * I / Gw;
-        const int slot = (lo_w / nK == tile) ? 2 * w : 2 * w + 1;
-        return reinterpret_cast<const f32x4*>(a.partial + (size_t)slot * (MT * PT)) + (size_t)(ml0 / 4) * PT + pl;
+        return reinterpret_cast<const f32x4*>(a.partial + (size_t)w * (MT * PT)) + (size_t)(ml0 / 4) * PT + pl;
     };
     float v[8];
     {
@@ -778,23 +769,33 @@ void x6_pack_weights(const float* w, int cout, int cin, int ks, int Mpad, int* n
         }
 }
 
-// number the groups' tiles (X6Group::t0, X6Args::tiles) for an MT x PT tile
+// number the groups' tiles and work units (X6Group::t0 / u0, X6Args::tiles / units) for an
+// MT x PT tile; slabs 0 counts as 1
 X6Args x6_number_tiles(const X6Args& a0, int mt, int pt) {
     X6Args a = a0;
     if (a.ngroups < 1 || a.ngroups > kX6Groups || a.Mpad % mt) throw std::invalid_argument("conv_x6: bad groups");
-    int t = 0;
+    int t = 0, u = 0;
     for (int g = 0; g < a.ngroups; ++g) {
-        if (a.g[g].npix <= 0) throw std::invalid_argument("conv_x6: empty group");
-        a.g[g].t0 = t;
-        t += (a.Mpad / mt) * ((a.g[g].npix + pt - 1) / pt);
+        X6Group& G = a.g[g];
+        if (G.npix <= 0) throw std::invalid_argument("conv_x6: empty group");
+        if (G.slabs < 1) G.slabs = 1;
+        if (G.slabs > a.nK || (a.pool && G.slabs != 1)) throw std::invalid_argument("conv_x6: bad slab count");
+        const int tg = (a.Mpad / mt) * ((G.npix + pt - 1) / pt);
+        G.t0 = t;
+        G.u0 = u;
+        t += tg;
+        u += tg * G.slabs;
     }
     a.tiles = t;
+    a.units = u;
     return a;
 }
 
 template <int MT, int PT>
 static void launch_x6_tile(const X6Args& a0, hipStream_t st) {
     const X6Args a = x6_number_tiles(a0, MT, PT);
+    if (a.sk_grid < 1 || a.sk_grid > a.units) throw std::invalid_argument("conv_x6: bad grid");
+    if ((size_t)a.units * MT * PT * 4 >= 0x7fffffffull) throw std::invalid_argument("conv_x6: too many slabs");
     const dim3 blk(64 * x6_waves(MT, PT));
     if (a.small != 0)
         hipLaunchKernelGGL((conv_x6<MT, PT, true, 0>), dim3(a.sk_grid), blk, 0, st, a);
@@ -806,7 +807,7 @@ static void launch_x6_tile(const X6Args& a0, hipStream_t st) {
         hipLaunchKernelGGL((conv_x6<MT, PT, false, 1>), dim3(a.sk_grid), blk, 0, st, a);
     else
         hipLaunchKernelGGL((conv_x6<MT, PT, false, 0>), dim3(a.sk_grid), blk, 0, st, a);
-    if (a.sk_grid != a.tiles)
+    if (a.units != a.tiles)
         hipLaunchKernelGGL((conv_x6_fixup<MT, PT>), dim3(a.tiles, MT * PT / 8 / 256), dim3(256), 0, st, a);
 }
 

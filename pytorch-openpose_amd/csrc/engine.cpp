@@ -23,6 +23,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <queue>
 #include <vector>
 
 #include "../../include/opose.h"
@@ -168,6 +169,10 @@ struct DevConv {
     // 3x3 / 7x7 layers: the same weights in pair order for conv_win_x6 (conv_win.hip)
     uint8_t* wx6p = nullptr;
     int nK6p = 0;
+    // k-slab policy inputs (engine slab_count): the network, the layer's resolution level
+    // (0: H .. 3: H/8) and whether it is one branch of a CPM pair (two GEMMs per launch)
+    int net = 0, lvl = 0;
+    bool pair = false;
     ~DevConv() {
         if (wx6) (void)hipFree(wx6);
         if (wx6p) (void)hipFree(wx6p);
@@ -241,12 +246,6 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_FUSE_1X1");
         return !(e && e[0] == '0');
     }();
-    // OPOSE_WIN_SK=0: conv_win_x6 only on data-parallel grids that fill the chip (no stream-K
-    // window launches; the A/B of the planner's window pricing)
-    bool win_dp_only = [] {
-        const char* e = getenv("OPOSE_WIN_SK");
-        return e && e[0] == '0';
-    }();
     // conv1_1 -> conv1_2 (window kernel) hand-off as fp32 units, split by conv1_2 (default);
     // OPOSE_C11_F32=0: as X6 (A/B, bit-identical)
     bool c11_f32 = [] {
@@ -265,9 +264,15 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_CONV12_WIN");
         return !(e && e[0] == '0');
     }();
-    // inside opose_body_band_maps: 1 (planner's grids), 2: OPOSE_BAND_DP (every conv on whole
-    // data-parallel tiles: each pixel's sum in one fixed order whatever the band); 0 otherwise
-    int band_win = 0;
+    // conv launch plans per launch signature (tile, grid) and the device copies of their unit
+    // schedules (X6Args::sched; never freed while the handle lives: captured graphs hold them)
+    struct ConvPlan {
+        int mt = 0, pt = 0, grid = 0;
+        int* sched = nullptr;
+    };
+    std::map<std::string, ConvPlan> plans;
+    std::vector<int*> sched_mem;
+    std::vector<std::vector<int>> sched_host;  // sources of the asynchronous uploads
     DevBuf frames, mids[2][kMaxScales], avg, cnt, list, peak_pos, part_cnt, score, conn, conn_cnt, records, maps_in,
         hlab, hsums, hpeaks, hfound, list_score, hsel;
     PinnedBuf hand_out;  // Hand() peaks + found, staged for the host
@@ -390,6 +395,7 @@ struct opose_ctx {
         }
         for (auto& kv : graphs)
             if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+        for (int* p : sched_mem) (void)hipFree(p);
         for (auto e : event_pool) (void)hipEventDestroy(e);
         if (own_stream) (void)hipStreamDestroy(own_stream);
     }
@@ -478,31 +484,56 @@ TileChoice choose_tile(int Mpad, const std::vector<int>& gpix, int nK, bool x6 =
     return best;
 }
 
-// conv_win_x6 (128 x 256 tiles, input window in LDS) priced in choose_tile's units: data parallel
-// when its rounds fill the chip, else stream-K over 256 workgroups.  `eff`: its cost per chunk
-// relative to conv_x6's 128 x 256 tile (fewer DMA instructions and LDS-DMA bytes).
-TileChoice choose_win(int Mpad, const std::vector<int>& gpix, int nK, double eff, double* cost_out) {
-    long tiles = 0;
-    for (int n : gpix) tiles += (long)(Mpad / 128) * ((n + 255) / 256);
-    const double unit = 8.0 * 0.4 * eff;
-    const long per_cu = (tiles + 255) / 256;
-    double best_cost = (double)per_cu * nK * unit;
-    TileChoice best{128, 256, (int)tiles};
-    const long iters = tiles * nK;
-    const long grid = std::min<long>(256, iters / 8);
-    if (grid >= 1 && grid != tiles) {
-        const double per_wg = (double)iters / grid;
-        const long segs = grid > 2 * tiles ? grid + tiles : std::min<long>(tiles, 2 * grid);
-        const double slab_bytes = grid > 2 * tiles ? (double)segs * 128 * 256 * 4.0 * 2.0 + (double)tiles * 128 * 256 * 4.0
-                                                   : (double)segs * 128 * 256 * 4.0 * 3.0;
-        const double sk = per_wg * unit + slab_bytes / 5e12 / 0.42e-6 + 8.0;
-        if (sk < best_cost * 0.97) {
-            best_cost = sk;
-            best = {128, 256, (int)grid};
-        }
+// ---------------------------------------------------------------- fixed k slabs (split-bf16 path)
+// A tile of a group with S slabs sums chunks [s nK / S, (s + 1) nK / S) from zero for each s and
+// the slabs are folded in slab order (common.h X6Group::slabs).  S is a function of the layer and
+// the segment (slab_count), so the work units (tile, slab) of a launch are fixed before its grid
+// is chosen; the grid only decides which workgroup runs which unit.
+
+struct SlabGroup {
+    long tiles;
+    int S;
+};
+
+// per-unit fixed cost in chunks (prologue: weight stages / window DMA; epilogue stores)
+constexpr double kUnitOvh = 1.5;
+
+// Longest-first assignment of the units of `gs` (numbered group, tile, slab) to G workgroups:
+// each unit costs its chunks + kUnitOvh and goes to the least loaded workgroup (ties: the lowest
+// index).  Returns the largest load in chunks; `lists`: per workgroup its units, ascending.
+double lpt_units(const std::vector<SlabGroup>& gs, int nK, int G, std::vector<std::vector<int>>* lists) {
+    struct Un {
+        double c;
+        int id;
+    };
+    std::vector<Un> us;
+    int u = 0;
+    double total = 0, big = 0;
+    for (const SlabGroup& g : gs)
+        for (long t = 0; t < g.tiles; ++t)
+            for (int s = 0; s < g.S; ++s, ++u) {
+                const double c = (double)((s + 1) * nK / g.S - s * nK / g.S) + kUnitOvh;
+                us.push_back({c, u});
+                total += c;
+                big = std::max(big, c);
+            }
+    if (!lists && us.size() > 8192) return std::max(total / G, big);  // planning estimate of a large launch
+    std::stable_sort(us.begin(), us.end(), [](const Un& a, const Un& b) { return a.c > b.c; });
+    std::priority_queue<std::pair<double, int>, std::vector<std::pair<double, int>>, std::greater<>> pq;
+    for (int w = 0; w < G; ++w) pq.push({0.0, w});
+    if (lists) lists->assign(G, {});
+    double mk = 0;
+    for (const Un& x : us) {
+        auto top = pq.top();
+        pq.pop();
+        top.first += x.c;
+        mk = std::max(mk, top.first);
+        if (lists) (*lists)[top.second].push_back(x.id);
+        pq.push(top);
     }
-    *cost_out = best_cost;
-    return best;
+    if (lists)
+        for (auto& L : *lists) std::sort(L.begin(), L.end());
+    return mk;
 }
 
 }  // namespace
@@ -516,6 +547,7 @@ struct Rccl {
     decltype(&ncclGetUniqueId) get_unique_id = nullptr;
     decltype(&ncclCommInitRank) comm_init_rank = nullptr;
     decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclCommAbort) comm_abort = nullptr;
     decltype(&ncclSend) send = nullptr;
     decltype(&ncclRecv) recv = nullptr;
     decltype(&ncclGroupStart) group_start = nullptr;
@@ -537,6 +569,7 @@ static const Rccl& rccl() {
         x.get_unique_id = reinterpret_cast<decltype(x.get_unique_id)>(sym("ncclGetUniqueId"));
         x.comm_init_rank = reinterpret_cast<decltype(x.comm_init_rank)>(sym("ncclCommInitRank"));
         x.comm_destroy = reinterpret_cast<decltype(x.comm_destroy)>(sym("ncclCommDestroy"));
+        x.comm_abort = reinterpret_cast<decltype(x.comm_abort)>(sym("ncclCommAbort"));
         x.send = reinterpret_cast<decltype(x.send)>(sym("ncclSend"));
         x.recv = reinterpret_cast<decltype(x.recv)>(sym("ncclRecv"));
         x.group_start = reinterpret_cast<decltype(x.group_start)>(sym("ncclGroupStart"));
@@ -571,6 +604,9 @@ static void upload_conv(opose_ctx* h, int net, const std::string& key, const std
     auto dc = std::make_unique<DevConv>();
     const Spec& s0 = *parts[0];
     dc->name = key;
+    dc->net = net;
+    dc->lvl = key.rfind("conv1_", 0) == 0 ? 0 : key.rfind("conv2_", 0) == 0 ? 1 : key.rfind("conv3_", 0) == 0 ? 2 : 3;
+    dc->pair = key.size() > 3 && (key.compare(key.size() - 3, 3, "_L1") == 0 || key.compare(key.size() - 3, 3, "_L2") == 0);
     dc->cin = s0.cin;
     dc->ks = s0.ks;
     dc->pad = s0.pad;
@@ -783,11 +819,15 @@ static XAct x6pact(uint8_t* p, int cg, int goff, int N, int H, int W) {
 }
 
 // One GEMM of a conv launch (an X6Group): a scale's frames through one branch's weights.
+// Hl: the frame height the k-slab policy sees (a row band's view passes its whole frame's rows;
+// 0: H); slabs: set by the planner (a frame view inherits its segment's).
 struct ConvSeg {
     DevConv* c;
     int N, H, W;
     XAct in, out, dup;  // dup: optional duplicate X6 destination
     bool relu;
+    int Hl = 0;
+    int slabs = 0;
 };
 
 // Run convs of one shape (ks, Cin, Mpad) over up to kX6Groups segments per launch: the CPM
@@ -805,54 +845,134 @@ static XAct frame_view(const XAct& a, int n, int H, int W) {
     return v;
 }
 
-// A multi-frame 7x7 segment on a padded input whose 256-pixel tiles straddle two frames with a window
-// larger than the LDS holds (a crop batch's largest pyramid scale: 2 x 92 x 92) would send
-// the whole launch to conv_x6: run such segments as one segment per frame (frame views of the
-// same buffers), whose windows fit, when the launch has group slots for them.
-static bool split_frames_for_win(const opose_ctx* h, const std::vector<ConvSeg>& segs, bool pool,
-                                 std::vector<ConvSeg>& out) {
-    if (!h->win7 || pool || segs.size() > (size_t)kX6Groups) return false;
-    size_t groups = 0;
-    bool any = false;
-    for (const ConvSeg& sg : segs) {
-        // 7x7 only: at 3x3 the per-crop windows measured slower than conv_x6 on the whole batch
-        // (conv3_x of two 368 crops 0.65 vs 0.62 ms), at 7x7 faster (0.24 vs 0.27 ms + fixups)
-        if (!sg.c->wx6p || !sg.in.padded || sg.c->ks != 7) return false;
-        if (conv_win_fits(sg.N, sg.H, sg.W, sg.c->ks)) {
-            ++groups;
-        } else if (sg.N > 1 && conv_win_fits(1, sg.H, sg.W, sg.c->ks)) {
-            groups += sg.N;
-            any = true;
-        } else {
-            return false;
-        }
-    }
-    if (!any || groups > (size_t)kX6Groups) return false;
-    out.clear();
-    for (const ConvSeg& sg : segs) {
-        if (conv_win_fits(sg.N, sg.H, sg.W, sg.c->ks)) {
-            out.push_back(sg);
-            continue;
-        }
-        for (int n = 0; n < sg.N; ++n)
-            out.push_back(ConvSeg{sg.c, 1, sg.H, sg.W, frame_view(sg.in, n, sg.H, sg.W),
-                                  frame_view(sg.out, n, sg.H, sg.W), frame_view(sg.dup, n, sg.H, sg.W), sg.relu});
-    }
-    return true;
+// The kernel family of a segment -- conv_x6's (4 groups, 1 tap) chunks or conv_win_x6's pair
+// order -- is part of each pixel's summation order, so like the slab count it is a function of
+// the layer and the segment only:
+//  * the window kernel for 3x3 / 7x7 layers on padded inputs whose window fits the LDS: one frame
+//    of any height (conv_win_fits_rows: a 256-pixel run at W columns, so a row band and its whole
+//    frame agree), or a batch whose tiles straddle frames;
+//  * a 7x7 batch whose straddling windows do not fit but one frame's do: the window kernel on
+//    one segment per frame (frame views of the same buffers; a crop batch's 92 x 92 scale);
+//  * body layers of fewer than 4096 pixels (C2's single frame, a pyramid's 0.5 scale): conv_x6,
+//    whose 128 x 64 tiles spread a small layer over the chip;
+//  * everything else (dense inputs, pooled convs, 1x1): conv_x6.
+enum { kKernelX6 = 0, kKernelWin = 1, kKernelWinFrames = 2 };
+static int seg_kernel(const opose_ctx* h, const ConvSeg& sg, bool pool) {
+    const DevConv* c = sg.c;
+    if (!h->win7 || pool || !c->wx6p || !sg.in.padded || (c->ks != 3 && c->ks != 7)) return kKernelX6;
+    const long lpix = (long)sg.N * (sg.Hl ? sg.Hl : sg.H) * sg.W;
+    if (c->net == OPOSE_NET_BODY && lpix < 4096) return kKernelX6;
+    if (sg.N == 1) return conv_win_fits_rows(sg.W, c->ks) ? kKernelWin : kKernelX6;
+    if (conv_win_fits(sg.N, sg.H, sg.W, c->ks)) return kKernelWin;
+    if (c->ks == 7 && h->split_frames && conv_win_fits_rows(sg.W, c->ks)) return kKernelWinFrames;
+    return kKernelX6;
 }
 
-static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, bool pool) {
-    if (segs.empty()) return;
-    {
-        std::vector<ConvSeg> per_frame;
-        if (h->split_frames && split_frames_for_win(h, segs, pool, per_frame)) return run_conv_x6_segs(h, per_frame, pool);
+// k slabs of a segment (common.h X6Group::slabs): a function of the layer, its kernel family and
+// the segment's logical geometry (N frames of H x W) -- never of the launch that runs it, its
+// grid, its other groups or a row band's rows.  Large layers keep one slab (one run over all
+// chunks, the data-parallel grids of the bench's 32-frame batch); smaller ones are cut so that
+// their work units fill the chip, counting tiles of the kernel's smallest tile (window: 128 x 256,
+// conv_x6: 128 x 64) and both branches of a CPM pair.  The hand's 7x7 / 3x3 layers run as one
+// launch per layer for a 4-scale pyramid (lockstep): their counts are set per scale size so that
+// the pyramid's units pack evenly over 256 workgroups (longest-first, lpt_units).
+static int slab_count(const DevConv* c, bool win, int N, int H, int W, bool pool) {
+    const int nK = win ? c->nK6p : c->nK6;
+    if (pool || nK < 8) return 1;
+    const int smax = nK / 4;
+    const long npix = (long)N * H * W;
+    const double mr = c->Mpad / 128.0;
+    auto clampS = [&](long s) { return (int)std::max<long>(1, std::min<long>(s, smax)); };
+    if (c->net == OPOSE_NET_HAND && win) {
+        const double T = std::ceil(npix / 256.0) * mr;
+        if (c->ks == 7) return clampS(T < 6 ? 16 : T < 12 ? 12 : T < 30 ? 8 : T < 60 ? 7 : T < 120 ? 4 : T < 240 ? 2 : 1);
+        return clampS(T < 12 ? 12 : T < 30 ? 6 : T < 60 ? 4 : T < 120 ? 2 : 1);
     }
-    if (segs.size() > (size_t)kX6Groups) {  // more scales x branches than one launch holds
-        for (size_t i = 0; i < segs.size(); i += kX6Groups)
-            run_conv_x6_segs(h, std::vector<ConvSeg>(segs.begin() + i, segs.begin() + std::min(segs.size(), i + kX6Groups)),
-                             pool);
-        return;
+    const int mult = c->pair ? 2 : 1;
+    if (win) {
+        const double T = std::ceil(npix / 256.0) * mr * mult;
+        return T >= 160 ? 1 : clampS(std::max(2L, std::lround(320.0 / T)));
     }
+    const double T = std::ceil(npix / 64.0) * mr * mult;
+    return T >= 640 ? 1 : clampS(std::max(2L, std::lround(384.0 / T)));
+}
+
+// conv_x6 tile configurations: mt, pt, co-resident workgroups per CU, cost per chunk relative to
+// a 64 x 64 tile's (measured, scripts/conv_timing.py; rounds 1-2)
+static const int kX6Cfg[6][3] = {{128, 128, 1}, {128, 256, 1}, {256, 128, 1}, {128, 64, 2}, {64, 128, 2}, {64, 64, 3}};
+static const double kX6Ovh[6] = {1.5, 1.0, 0.96, 1.1, 1.1, 1.2};
+
+// Launch plan of one kernel family over segments whose slab counts are set: tile shape, grid,
+// and (units > grid or unequal units) the longest-first unit schedule.  Cached per signature.
+static opose_ctx::ConvPlan plan_launch(opose_ctx* h, const std::vector<ConvSeg>& segs, bool win, bool pool, int nK,
+                                       int Mpad) {
+    std::string key = (win ? "w" : "x") + std::to_string(pool) + "/" + std::to_string(nK) + "/" + std::to_string(Mpad);
+    for (const ConvSeg& s : segs)
+        key += "/" + std::to_string((long)s.N * s.H * s.W) + ":" + std::to_string(s.slabs) + ":" +
+               std::to_string(pool ? s.W : 0);
+    auto it = h->plans.find(key);
+    if (it != h->plans.end()) return it->second;
+    auto groups_for = [&](int mt, int pt) {
+        std::vector<SlabGroup> gs;
+        for (const ConvSeg& s : segs) {
+            const long np = pool ? (long)s.N * (s.H / 2) * (s.W / 2) * 4 : (long)s.N * s.H * s.W;
+            gs.push_back({(long)(Mpad / mt) * ((np + pt - 1) / pt), s.slabs});
+        }
+        return gs;
+    };
+    bool multi = false;
+    for (const ConvSeg& s : segs) multi = multi || s.slabs > 1;
+    opose_ctx::ConvPlan best;
+    double best_cost = 1e300;
+    for (int ci = 0; ci < 6; ++ci) {
+        const int mt = win ? 128 : kX6Cfg[ci][0], pt = win ? 256 : kX6Cfg[ci][1], occ = win ? 1 : kX6Cfg[ci][2];
+        if (win && ci > 0) break;
+        if (Mpad % mt) continue;
+        const std::vector<SlabGroup> gs = groups_for(mt, pt);
+        long units = 0, tiles = 0;
+        for (const SlabGroup& g : gs) {
+            units += g.tiles * g.S;
+            tiles += g.tiles;
+        }
+        // one-slab launches: one workgroup per tile, the hardware dispatcher balancing them
+        const long G = multi ? std::min<long>(units, 256L * occ) : tiles;
+        const double mk = multi ? lpt_units(gs, nK, (int)G, nullptr) : (double)((tiles + 256L * occ - 1) / (256L * occ)) * nK;
+        const double unit = (mt / 64.0) * (pt / 64.0) * (win ? 0.8 : kX6Ovh[ci]) * 0.4;
+        // co-resident workgroups share a CU; a lone one of a 2-3 per CU tile runs at ~60 %
+        const double share = G <= 256 ? (occ >= 2 ? 1.6 : 1.0) : (multi ? std::min<double>(occ, (double)G / 256.0) : occ);
+        double cost = mk * unit * share;
+        if (multi) cost += (double)units * mt * pt * 4.0 * 2.0 / 5e12 / 0.42e-6 + 8.0;  // slab partials + fixup
+        if (cost < best_cost * 0.97) {
+            best_cost = cost;
+            best.mt = mt;
+            best.pt = pt;
+            best.grid = (int)G;
+        }
+    }
+    best.sched = nullptr;
+    if (multi) {
+        std::vector<std::vector<int>> lists;
+        lpt_units(groups_for(best.mt, best.pt), nK, best.grid, &lists);
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        OPOSE_HIP_CHECK(hipStreamIsCapturing(h->stream, &cs));
+        if (cs != hipStreamCaptureStatusNone) return best;  // (captured: contiguous unit ranges, same sums)
+        std::vector<int> flat(best.grid + 1, 0);
+        for (int w = 0; w < best.grid; ++w) flat[w + 1] = flat[w] + (int)lists[w].size();
+        for (const auto& L : lists) flat.insert(flat.end(), L.begin(), L.end());
+        int* d = nullptr;
+        OPOSE_HIP_CHECK(hipMalloc(&d, flat.size() * sizeof(int)));
+        h->sched_host.push_back(std::move(flat));
+        const std::vector<int>& src = h->sched_host.back();
+        OPOSE_HIP_CHECK(hipMemcpyAsync(d, src.data(), src.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+        h->sched_mem.push_back(d);
+        best.sched = d;
+    }
+    h->plans[key] = best;
+    return best;
+}
+
+// One launch: segments of one kernel family, at most kX6Groups of them, slab counts set.
+static void launch_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, bool win, bool pool) {
     DevConv* c0 = segs[0].c;
     X6Args a{};
     const int ng = (int)segs.size();
@@ -860,25 +980,23 @@ static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, boo
     a.pad = c0->pad;
     a.cin_g = c0->cin_g;
     a.small = c0->small6 ? 1 : 0;
-    a.nK = c0->nK6;
+    a.nK = win ? c0->nK6p : c0->nK6;
     a.Mpad = c0->Mpad;
     a.pool = pool ? 1 : 0;
     a.ngroups = ng;
-    std::vector<int> gpix;
-    bool win_ok = h->win7 && !pool;
     double flops = 0;
     long npix_all = 0;
     for (int g = 0; g < ng; ++g) {
         const ConvSeg& sg = segs[g];
         DevConv* c = sg.c;
-        if (c->ks != c0->ks || c->cin_g != c0->cin_g || c->Mpad != c0->Mpad || c->nK6 != c0->nK6)
+        if (c->ks != c0->ks || c->cin_g != c0->cin_g || c->Mpad != c0->Mpad || c->nK6 != c0->nK6 || c->nK6p != c0->nK6p)
             throw std::invalid_argument("conv segments of different shapes");
         if (pool && (sg.dup.p || sg.out.f32)) throw std::invalid_argument("pooled conv: single X6 output only");
         X6Group& G = a.g[g];
         G.in = static_cast<const uint8_t*>(sg.in.p);
         G.in_ps = sg.in.ps;
         G.in_l = sg.in.l;
-        G.wt = c->wx6;
+        G.wt = win ? c->wx6p : c->wx6;
         G.bias = c->bias;
         G.out = sg.out.p;
         G.out_ps = sg.out.ps;
@@ -897,66 +1015,59 @@ static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, boo
         G.npix = pool ? sg.N * (sg.H / 2) * (sg.W / 2) * 4 : sg.N * sg.H * sg.W;
         G.ylo = sg.in.ylo;
         G.yhi = sg.in.yhi;
+        G.slabs = sg.slabs;
         if (G.yhi && (sg.N != 1 || pool)) throw std::invalid_argument("row band views: one frame, no pooling");
-        gpix.push_back(G.npix);
         npix_all += G.npix;
         flops += 2.0 * c->cout * (double)c->K * (pool ? 4.0 * sg.N * (sg.H / 2) * (sg.W / 2) : (double)G.npix);
-        win_ok = win_ok && c->wx6p && sg.in.padded && conv_win_fits(sg.N, sg.H, sg.W, c->ks);
     }
-    // pooled convs run whole tiles (data parallel): price only those
-    double cost = 0;
-    TileChoice t = choose_tile(a.Mpad, gpix, a.nK, true, pool, &cost);
-    if (pool) t.grid = x6_number_tiles(a, t.mt, t.pt).tiles;
-    // 3x3 / 7x7 layers on padded inputs: the LDS-window kernel when it prices lower (its chunk
-    // costs ~0.8 of conv_x6's at 7x7 -- 290 vs 262 TF/s on the bench's 236-tile grids, 225 vs
-    // 200 TF/s stream-K on a hand crop's pyramid -- and ~0.95 at 3x3)
-    std::string kind = "x6";
-    if (win_ok && !h->win_dp_only) {
-        double wcost = 0;
-        const TileChoice tw = choose_win(a.Mpad, gpix, c0->nK6p, c0->ks == 7 ? 0.8 : 0.95, &wcost);
-        if (wcost < cost) {
-            t = tw;
-            kind = "win";
-        }
-    } else if (win_ok) {  // OPOSE_WIN_SK=0: the window kernel only on data-parallel grids that fill the chip
-        long tiles = 0;
-        for (int n : gpix) tiles += (long)(a.Mpad / 128) * ((n + 255) / 256);
-        const double fill = (double)tiles / (double)(((tiles + 255) / 256) * 256);
-        if (tiles >= 192 && fill >= 0.85) {
-            t = TileChoice{128, 256, (int)tiles};
-            kind = "win";
-        }
-    }
-    if (h->band_win == 2) {  // OPOSE_BAND_DP: whole tiles, the same per-pixel sum in any band
-        long tiles = 0;
-        if (win_ok) {
-            for (int n : gpix) tiles += (long)(a.Mpad / 128) * ((n + 255) / 256);
-            t = TileChoice{128, 256, (int)tiles};
-            kind = "win";
-        } else {
-            t = choose_tile(a.Mpad, gpix, a.nK, true, true, &cost);
-            kind = "x6";
-        }
-    }
-    a.sk_grid = t.grid;
-    a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+    const opose_ctx::ConvPlan p = plan_launch(h, segs, win, pool, a.nK, a.Mpad);
+    a.sk_grid = p.grid;
+    a.sched = p.sched;
+    const X6Args num = x6_number_tiles(a, p.mt, p.pt);
+    a.partial = num.units != num.tiles ? h->w().partial.ensure<float>((size_t)num.units * p.mt * p.pt, h->stream) : nullptr;
     ProfEntry pe;
     h->prof_begin(pe, conv_class(c0->ks), flops, 0);
     if (h->detail) {
         std::string nm = c0->name;
         for (int g = 1; g < ng; ++g)
             if (segs[g].c != c0 && nm.find(segs[g].c->name) == std::string::npos) nm += "|" + segs[g].c->name;
-        pe.detail = "layer/" + nm + "/" + kind + "/" + std::to_string(t.mt) + "x" + std::to_string(t.pt) + "s" +
-                    std::to_string(t.grid) + "/g" + std::to_string(ng) + "/n" + std::to_string(npix_all);
+        pe.detail = "layer/" + nm + "/" + (win ? "win" : "x6") + "/" + std::to_string(p.mt) + "x" + std::to_string(p.pt) +
+                    "g" + std::to_string(p.grid) + "u" + std::to_string(num.units) + "/g" + std::to_string(ng) + "/n" +
+                    std::to_string(npix_all);
     }
-    if (kind == "win") {
-        a.nK = c0->nK6p;
-        for (int g = 0; g < ng; ++g) a.g[g].wt = segs[g].c->wx6p;
-        launch_conv_win_x6(a, h->stream);
-    } else {
-        launch_conv_x6(a, t.mt, t.pt, h->stream);
-    }
+    if (win) launch_conv_win_x6(a, h->stream);
+    else launch_conv_x6(a, p.mt, p.pt, h->stream);
     h->prof_end(pe);
+}
+
+static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, bool pool) {
+    if (segs.empty()) return;
+    // kernel family and slab count per segment, frames of kKernelWinFrames segments as segments
+    std::vector<ConvSeg> parts[2];
+    for (const ConvSeg& s0 : segs) {
+        ConvSeg sg = s0;
+        const int kind = seg_kernel(h, sg, pool);
+        const bool win = kind != kKernelX6;
+        if (!sg.slabs) sg.slabs = slab_count(sg.c, win, sg.N, sg.Hl ? sg.Hl : sg.H, sg.W, pool);
+        if (kind == kKernelWinFrames) {
+            for (int n = 0; n < sg.N; ++n) {
+                ConvSeg f = sg;
+                f.N = 1;
+                f.in = frame_view(sg.in, n, sg.H, sg.W);
+                f.out = frame_view(sg.out, n, sg.H, sg.W);
+                f.dup = frame_view(sg.dup, n, sg.H, sg.W);
+                parts[1].push_back(f);
+            }
+        } else {
+            parts[win ? 1 : 0].push_back(sg);
+        }
+    }
+    for (int k = 0; k < 2; ++k)
+        for (size_t i = 0; i < parts[k].size(); i += kX6Groups)
+            launch_segs(h,
+                        std::vector<ConvSeg>(parts[k].begin() + i,
+                                             parts[k].begin() + std::min(parts[k].size(), i + (size_t)kX6Groups)),
+                        k == 1, pool);
 }
 
 // A CPM stage's closing 1x1 pair (conv5_4 -> conv5_5, conv6_1 -> conv6_2, Mconv6 -> Mconv7) on one
@@ -967,6 +1078,7 @@ struct ChainSeg {
     int N, H, W;
     XAct in, mid, out;
     bool relu2;
+    int Hl = 0;  // ConvSeg::Hl of the two-launch form
 };
 
 // One launch of conv1x1_chain_x6 for every segment (the intermediate never leaves the CU), or,
@@ -983,8 +1095,8 @@ static void run_chain_x6(opose_ctx* h, const std::vector<ChainSeg>& segs) {
     if (!fuse) {
         std::vector<ConvSeg> first, second;
         for (const ChainSeg& sg : segs) {
-            first.push_back(ConvSeg{sg.c1, sg.N, sg.H, sg.W, sg.in, sg.mid, XAct{}, true});
-            second.push_back(ConvSeg{sg.c2, sg.N, sg.H, sg.W, sg.mid, sg.out, XAct{}, sg.relu2});
+            first.push_back(ConvSeg{sg.c1, sg.N, sg.H, sg.W, sg.in, sg.mid, XAct{}, true, sg.Hl});
+            second.push_back(ConvSeg{sg.c2, sg.N, sg.H, sg.W, sg.mid, sg.out, XAct{}, sg.relu2, sg.Hl});
         }
         run_conv_x6_segs(h, first);
         run_conv_x6_segs(h, second);
@@ -1075,6 +1187,7 @@ struct NetSeg {
     const float* x;  // [N][3][Hp][Wp] fp32 network input
     int N, Hp, Wp;
     int slot;  // workspace set (opose_ctx::ws)
+    int Hl = 0;  // the whole frame's input rows when x is a row band's rows (ConvSeg::Hl); 0: Hp
 };
 
 static void run_scales_concurrently(opose_ctx* h, int ns, const std::function<void(int)>& fn);
@@ -1222,7 +1335,7 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
             const XAct out = fuse ? out_buf(i, lvl + 1, og) : final_layer ? last[i] : out_buf(i, lvl, og);
             outs.push_back(out);
             cs.push_back(ConvSeg{c, sg.N, sg.Hp >> lvl, sg.Wp >> lvl, bs[i].cur, out,
-                                 final_layer && !fuse ? dup[i] : XAct{}, true});
+                                 final_layer && !fuse ? dup[i] : XAct{}, true, sg.Hl >> lvl});
         }
         run_conv_x6_segs(h, cs, fuse);
         for (size_t i = 0; i < ns; ++i) bs[i].cur = outs[i];
@@ -1253,7 +1366,10 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
 // Output rows [r0, r1) of one frame's CPM stages (opose_body_band_maps).  The stage buffers keep
 // the whole frame's geometry; every stage layer runs on a view of the band's rows (X6P origin
 // moved down r0 rows), whose padding rows are the neighbouring bands' rows: band_halo refreshes
-// them before each 3x3 / 7x7 layer that reads them.  The trunk before the stages runs whole.
+// them before each 3x3 / 7x7 layer that reads them.  The trunk before the stages runs on the
+// band's rows plus kBandTrunkMargin rows past each cut (recomputed, not exchanged).  Every conv of
+// the band sums each pixel in the order of the whole frame's (ConvSeg::Hl = the frame's rows), so
+// the band's maps are the whole frame's rows bit for bit.
 struct Band {
     int r0, r1;
     float* maps;  // [57][r1 - r0][wl] fp32 device
@@ -1362,8 +1478,8 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
         DevConv* c2 = n2.empty() ? nullptr : find_conv(h, net, n2);
         std::vector<ConvSeg> cs;
         for (size_t i = 0; i < ns; ++i) {
-            cs.push_back(ConvSeg{c1, bs[i].N, rows(i), bs[i].wl, in1(i), out1(i), XAct{}, relu1});
-            if (c2) cs.push_back(ConvSeg{c2, bs[i].N, rows(i), bs[i].wl, in2(i), out2(i), XAct{}, relu2});
+            cs.push_back(ConvSeg{c1, bs[i].N, rows(i), bs[i].wl, in1(i), out1(i), XAct{}, relu1, bs[i].hl});
+            if (c2) cs.push_back(ConvSeg{c2, bs[i].N, rows(i), bs[i].wl, in2(i), out2(i), XAct{}, relu2, bs[i].hl});
         }
         run_conv_x6_segs(h, cs);
     };
@@ -1384,7 +1500,7 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
             v.l.fs = (uint32_t)(b - a + 3) * v.l.rs;
             return v;
         };
-        run_trunk_x6(h, net, {NetSeg{xs, 1, Hs, Wp, segs[0].slot}}, {sub(last[0])}, {sub(dup[0])});
+        run_trunk_x6(h, net, {NetSeg{xs, 1, Hs, Wp, segs[0].slot, Hp}}, {sub(last[0])}, {sub(dup[0])});
     } else {
         run_trunk_x6(h, net, segs, last, dup);
     }
@@ -1413,7 +1529,7 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
     chain("conv5_4_CPM_L1", "conv5_5_CPM_L1", "conv5_4_CPM_L2", "conv5_5_CPM_L2",
           [&](size_t i, int br, DevConv* c1, DevConv* c2) {
               return ChainSeg{c1, c2, bs[i].N, rows(i), bs[i].wl, t_(i, 0, br ? 16 : 0), u_(i, br ? 64 : 0),
-                              s_(i, 1, br ? 5 : 0), false};
+                              s_(i, 1, br ? 5 : 0), false, bs[i].hl};
           });
     band_halo(bs[0].S[1], SG, 0, 8);
     int cur = 1;
@@ -1437,7 +1553,7 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
                   const XAct o = st < 6 ? s_(i, cur ^ 1, br ? 5 : 0)
                                  : band ? f32act(band->maps, 57, br ? 38 : 0) : f32act(bs[i].O, 185, br ? 38 : 0);
                   return ChainSeg{c1, c2, bs[i].N, rows(i), bs[i].wl, t_(i, t, br ? 16 : 0), t_(i, t ^ 1, br ? 16 : 0), o,
-                                  br == 1 && st == 6};
+                                  br == 1 && st == 6, bs[i].hl};
               });
         if (st < 6) band_halo(bs[0].S[cur ^ 1], SG, 0, 8);  // the next Mconv1 (7x7) reads them
         cur ^= 1;
@@ -2402,6 +2518,19 @@ int opose_rccl_init(opose_t* h, const void* id, int rank, int nranks) {
     });
 }
 
+int opose_rccl_abort(opose_t* h) {
+    if (!h) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        if (h->comm) {
+            ncclComm_t c = h->comm;
+            h->comm = nullptr;
+            h->band_up = h->band_dn = -1;
+            rccl_check(rccl().comm_abort(c));
+        }
+        return OPOSE_OK;
+    });
+}
+
 int opose_set_band_peers(opose_t* h, int up, int dn) {
     if (!h) return OPOSE_E_ARG;
     h->band_up = up;
@@ -2440,11 +2569,6 @@ int opose_body_band_maps(opose_t* h, const uint8_t* bgr, int H, int W, int64_t r
                           (float)p.pad_value / 256.f - 0.5f, x, h->stream);
         const size_t cap = xbuf_bytes / 4;
         const Band band{r0, r1, out, fn, user, static_cast<uint8_t*>(xbuf), cap};
-        struct BandWin {  // the band's grid policy for this call only, also when it throws
-            opose_ctx* h;
-            ~BandWin() { h->band_win = 0; }
-        } band_win_reset{h};
-        h->band_win = (flags & OPOSE_BAND_DP) ? 2 : 1;
         body_net_x6(h, {NetSeg{x, 1, g.Hp, g.Wp, h->slot}}, &band);
         if (!(flags & OPOSE_OUT_DEVICE)) {
             OPOSE_HIP_CHECK(hipMemcpyAsync(maps, out, (size_t)57 * hb * g.wl * 4, hipMemcpyDeviceToHost, h->stream));
@@ -2892,6 +3016,27 @@ int opose_debug_conv(opose_t* h, const float* x, const float* w, const float* b,
     return OPOSE_OK;
 }
 
+// Test-hook plan of a conv_x6 launch (groups filled): tile mt x pt (0: choose_tile's data-parallel
+// pick), `slabs` k slabs per tile (<= 1: one; clamped to nK), one workgroup per whole tile or,
+// with slabs, min(units, 256) workgroups over contiguous unit ranges; sets grid, units, partials.
+static TileChoice debug_x6_plan(opose_ctx* h, X6Args& a, int mt, int pt, int slabs) {
+    std::vector<int> gpix;
+    for (int g = 0; g < a.ngroups; ++g) gpix.push_back(a.g[g].npix);
+    TileChoice t = choose_tile(a.Mpad, gpix, a.nK, true, true);
+    if (mt > 0) {
+        t.mt = mt;
+        t.pt = pt;
+    }
+    if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
+    for (int g = 0; g < a.ngroups; ++g) a.g[g].slabs = std::max(1, std::min(slabs, a.nK));
+    const X6Args num = x6_number_tiles(a, t.mt, t.pt);
+    t.grid = num.units == num.tiles ? num.tiles : std::min(num.units, 256);
+    a.sk_grid = t.grid;
+    a.sched = nullptr;
+    a.partial = h->w().partial.ensure<float>((size_t)num.units * t.mt * t.pt, h->stream);
+    return t;
+}
+
 // split-bf16 conv of one layer: x fp32 NCHW -> X6 -> conv_x6 -> fp32 (out_x6: through an X6
 // output buffer and back, exercising the split epilogue)
 int opose_debug_conv_x6(opose_t* h, const float* x, const float* w, const float* b, int N, int Cin, int H, int W,
@@ -2922,13 +3067,8 @@ int opose_debug_conv_x6(opose_t* h, const float* x, const float* w, const float*
         G.wt = c->wx6; G.bias = c->bias; G.cout = Cout; G.relu = relu; G.out2 = nullptr;
         if (out_x6) { G.out = y6; G.out_ps = ops; G.out_l = x6act(y6, og, 0, N, H, W).l; G.out_f32 = 0; }
         else { G.out = yd; G.out_c = Cout; G.out_off = 0; G.out_f32 = 1; }
-        TileChoice t = choose_tile(a.Mpad, {G.npix}, a.nK, true);
-        if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((G.npix + pt - 1) / pt); }
-        if (splits > 0) t.grid = splits;
-        if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
         a.ngroups = 1;
-        a.sk_grid = t.grid;
-        a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        const TileChoice t = debug_x6_plan(h, a, mt, pt, splits);
         launch_conv_x6(a, t.mt, t.pt, h->stream);
         if (out_x6) launch_from_x6(y6, og, 0, ops, Cout, N, HW, yd, Cout, 0, h->stream);
         OPOSE_HIP_CHECK(hipMemcpyAsync(out, yd, ny * 4, hipMemcpyDeviceToHost, h->stream));
@@ -2971,13 +3111,8 @@ int opose_debug_conv_x6_time(opose_t* h, int N, int Cin, int H, int W, int Cout,
             G.out = y6 + (size_t)gg * N * og * HW * 16; G.out_ps = ops; G.out_l = x6act(y6, og, 0, N, H, W).l;
             G.out_f32 = 0;
         }
-        TileChoice t = choose_tile(a.Mpad, std::vector<int>(ngroups, N * HW), a.nK, true);
-        if (mt > 0) { t.mt = mt; t.pt = pt; t.grid = (a.Mpad / mt) * ((N * HW + pt - 1) / pt) * ngroups; }
-        if (splits > 0) t.grid = splits;
-        if (a.Mpad % t.mt) throw std::invalid_argument("tile M does not divide Mpad");
         a.ngroups = ngroups;
-        a.sk_grid = t.grid;
-        a.partial = h->w().partial.ensure<float>((size_t)2 * t.grid * t.mt * t.pt, h->stream);
+        const TileChoice t = debug_x6_plan(h, a, mt, pt, splits);
         launch_conv_x6(a, t.mt, t.pt, h->stream);  // warm-up
         hipEvent_t e0, e1;
         OPOSE_HIP_CHECK(hipEventCreate(&e0));

@@ -30,9 +30,10 @@ void launch_maxpool(const float* in, float* out, int NC, int H, int W, hipStream
 // conv_x6.hip (split-bf16 fp32-accurate convolution, X6 activation format: common.h)
 void x6_pack_weights(const float* w, int cout, int cin, int ks, int Mpad, int* nK_out, std::vector<uint16_t>& out);
 void launch_conv_x6(const X6Args& a, int mt, int pt, hipStream_t st);
-// X6Args with the groups' tiles numbered for an mt x pt tile (X6Group::t0, X6Args::tiles)
+// X6Args with the groups' tiles and work units numbered for an mt x pt tile (X6Group::t0 / u0,
+// X6Args::tiles / units)
 X6Args x6_number_tiles(const X6Args& a, int mt, int pt);
-// stream-K fixup of a 128 x 256 tile grid (conv_win_x6)
+// slab fixup of a 128 x 256 tile grid (conv_win_x6)
 void launch_conv_x6_fixup(const X6Args& a, int mt, int pt, hipStream_t st);
 void launch_to_x6(const float* in, int cstride, int coff, int C, int N, int HW, uint8_t* out, int cg, int goff,
                   uint32_t ps, hipStream_t st);
@@ -57,11 +58,13 @@ void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int
 // conv1x1_chain.hip: two chained 1x1 convs (CPM stage ends) in one launch, 64-pixel tiles
 void launch_conv1x1_chain_x6(const X6ChainArgs& a, hipStream_t st);
 // conv_win.hip: the 7x7 / 3x3 convs with the im2col operand from an LDS window of the padded X6P
-// input (pair-order weights: x6_pack_weights_pairs); 128 x 256 tiles, data parallel
-// (sk_grid == tiles) or stream-K
+// input (pair-order weights: x6_pack_weights_pairs); 128 x 256 tiles, work units (tile, k slab)
 void x6_pack_weights_pairs(const float* w, int cout, int cin, int ks, int Mpad, int* nK_out,
                            std::vector<uint16_t>& out);
+// the windows of an N x H x W batch's tiles fit the LDS
 bool conv_win_fits(int N, int H, int W, int ks);
+// the window of any 256-pixel run of one frame W columns wide fits the LDS (whatever the height)
+bool conv_win_fits_rows(int W, int ks);
 void launch_conv_win_x6(const X6Args& a, hipStream_t st);
 // imgproc.hip
 void launch_preprocess(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int Hs,

@@ -48,8 +48,8 @@ __device__ __forceinline__ void store4_x6(uint8_t* unit, uint32_t ps, const floa
     }
 }
 
-// Stream-K partial slabs (X6Args::partial): per workgroup piece an fp32 [MT/4][PT] array of
-// channel quads -- quad q (channels 4q .. 4q+3 of the tile), pixel pl at float index
+// Slab partials (X6Args::partial): per work unit of a multi-slab group an fp32 [MT/4][PT] array
+// of channel quads -- quad q (channels 4q .. 4q+3 of the tile), pixel pl at float index
 // (q * PT + pl) * 4.  A lane's accumulator block holds 4 consecutive channels of one pixel, so
 // it leaves the kernel as one 16-byte write-through (sc1) store; conv_x6_fixup reads two quads
 // per X6 unit.
@@ -71,6 +71,30 @@ __device__ __forceinline__ int x6_group_of(const X6Args& a, int tile) {
     int g = 0;
     for (int i = 1; i < a.ngroups; ++i) g = tile >= a.g[i].t0 ? i : g;
     return g;
+}
+
+// A work unit: chunks [c0, c1) of one tile, slab s of the group's `slabs` (common.h X6Group)
+struct X6Unit {
+    int g, tile, c0, c1;
+    bool whole;  // the tile's only slab: the conv writes the output itself
+};
+__device__ __forceinline__ X6Unit x6_unit_of(const X6Args& a, int u) {
+    int g = 0;
+    for (int i = 1; i < a.ngroups; ++i) g = u >= a.g[i].u0 ? i : g;
+    const int S = a.g[g].slabs, ul = u - a.g[g].u0, tl = ul / S, s = ul - tl * S;
+    return X6Unit{g, a.g[g].t0 + tl, s * a.nK / S, (s + 1) * a.nK / S, S == 1};
+}
+
+// the unit list of workgroup w of gridDim.x: positions [k0, k1) of `list` (nullptr: the units
+// themselves, a contiguous range)
+struct X6Work {
+    int k0, k1;
+    const int* list;
+};
+__device__ __forceinline__ X6Work x6_work_of(const X6Args& a, int w) {
+    const int G = gridDim.x;
+    if (a.sched) return X6Work{a.sched[w], a.sched[w + 1], a.sched + G + 1};
+    return X6Work{(int)((long long)w * a.units / G), (int)((long long)(w + 1) * a.units / G), nullptr};
 }
 
 }  // namespace x6

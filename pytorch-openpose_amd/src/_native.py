@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("OPOSE_LIB", os.path.join(os.path.dirname(_HERE), "lib
 OPOSE_OK = 0
 OPOSE_E_ARG, OPOSE_E_SHAPE, OPOSE_E_HIP, OPOSE_E_WEIGHTS, OPOSE_E_CAPACITY, OPOSE_E_ASSEMBLY = -1, -2, -3, -4, -5, -6
 NET_BODY, NET_HAND = 0, 1
-IN_DEVICE, OUT_DEVICE, PIPELINE, BAND_DP = 1, 2, 4, 8
+IN_DEVICE, OUT_DEVICE, PIPELINE = 1, 2, 4
 MAX_SCALES = 8
 
 
@@ -60,6 +60,7 @@ def _load():
         "opose_body_band_halo_bytes": (S, [I]),
         "opose_rccl_unique_id": (I, [P, S]),
         "opose_rccl_init": (I, [P, P, I, I]),
+        "opose_rccl_abort": (I, [P]),
         "opose_set_band_peers": (I, [P, I, I]),
         "opose_body_band_maps": (I, [P, P, I, I, C.c_int64, C.POINTER(Params), I, I, I, P, HALO_FN, P, P, S, I]),
         "opose_hand_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, P, I]),
@@ -98,7 +99,7 @@ EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last
             "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_hand_forward_pyramid",
             "opose_body_infer",
             "opose_body_post", "opose_body_scale_geom", "opose_body_scale_maps",
-            "opose_body_post_scales", "opose_body_band_halo_bytes", "opose_body_band_maps", "opose_rccl_unique_id", "opose_rccl_init", "opose_set_band_peers", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
+            "opose_body_post_scales", "opose_body_band_halo_bytes", "opose_body_band_maps", "opose_rccl_unique_id", "opose_rccl_init", "opose_rccl_abort", "opose_set_band_peers", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
             "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_conv_time", "opose_debug_conv_x6", "opose_debug_conv_x6_time", "opose_debug_preprocess",
             "opose_debug_heat", "opose_debug_hand_label"]
 
@@ -202,6 +203,10 @@ class Handle:
     def rccl_init(self, uid: bytes, rank: int, nranks: int):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid[:128])
         self.check(lib.opose_rccl_init(self.h, buf, int(rank), int(nranks)))
+
+    def rccl_abort(self):
+        """ncclCommAbort on the band communicator (a failed band rank's neighbours stop waiting)."""
+        self.check(lib.opose_rccl_abort(self.h))
 
     def set_band_peers(self, up, dn):
         self.check(lib.opose_set_band_peers(self.h, -1 if up is None else int(up), -1 if dn is None else int(dn)))

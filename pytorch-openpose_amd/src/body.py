@@ -136,7 +136,7 @@ class Body(object):
             maps.ctypes.data, 0))
         return maps
 
-    def band_maps(self, frame, s, r0, r1, exchange=None, exact=False):
+    def band_maps(self, frame, s, r0, r1, exchange=None):
         """Rows [r0, r1) of scale `s`'s network maps for one frame: [1, 57, r1-r0, wl] float32
         (opose_body_band_maps; src/body.py:36-50 for one m, cut into output rows).
 
@@ -147,7 +147,8 @@ class Body(object):
         hipStream_t, on which the send halves are being packed.  Not needed when one band covers
         every row.  exchange="rccl": the library's own RCCL send/recv on its stream, with the
         communicator and neighbours of src.dist.init_band_comm / Handle.set_band_peers (no Python
-        between the layers).  exact: whole data-parallel tiles (bit-identical to any banding)."""
+        between the layers).  The bands of a frame put together are scale_maps(frame, s) bit for
+        bit: every conv sums a pixel in the whole frame's order."""
         import torch
         dev = hasattr(frame, "data_ptr")
         if dev:
@@ -179,7 +180,7 @@ class Body(object):
                 return 1
 
         cb = _native.HALO_FN() if exchange == "rccl" else _native.HALO_FN(_cb)  # NULL: the library's RCCL
-        flags = _native.BAND_DP if exact else 0
+        flags = 0
         if dev:
             out = torch.empty((1, 57, r1 - r0, wl), dtype=torch.float32, device=frame.device)
             self.handle.wait_torch()

@@ -15,6 +15,9 @@ a single all_gather over xGMI (RCCL = torch.distributed 'nccl' on ROCm) per batc
 """
 from __future__ import annotations
 
+import functools
+import itertools
+
 import torch
 import torch.distributed as dist
 
@@ -103,6 +106,9 @@ def band_rows(hl: int, nb: int):
     return [(hl * i // nb, hl * (i + 1) // nb) for i in range(nb)]
 
 
+MAX_PLAN_COMBOS = 4096  # band-count combinations split_plan searches (the largest scales first)
+
+
 def split_plan(costs, world: int, hls=None, trunk_frac: float = TRUNK_FRAC, overhead: float = BAND_OVERHEAD):
     """Balanced single-frame split of a scale pyramid over `world` ranks.
 
@@ -111,14 +117,27 @@ def split_plan(costs, world: int, hls=None, trunk_frac: float = TRUNK_FRAC, over
     Returns (order, owners, load): owners[s] = ranks of scale s's bands, top to bottom (one rank:
     the whole scale); every rank runs its pieces in `order` (scales by decreasing piece cost, the
     same order everywhere, so the band groups' halo exchanges cannot wait on each other in a
-    cycle); load[r] = modelled work of rank r.  Exhaustive over band counts (world^n_scales
-    combinations, <= 4096 at 8 ranks and 4 scales), pieces placed largest-first on the least
-    loaded distinct ranks; ties keep fewer bands."""
-    import itertools
+    cycle); load[r] = modelled work of rank r.  Searches the band counts of the largest scales
+    exhaustively -- as many scales as keep the search within MAX_PLAN_COMBOS combinations (all
+    four of C5 up to 8 ranks: 8^4 = 4096); smaller scales stay whole -- pieces placed
+    largest-first on the least loaded distinct ranks; ties keep fewer bands.  The plan is a pure
+    function of its arguments and is cached, so a video's frames pay for the search once."""
+    order, owners, load = _split_plan(tuple(costs), int(world), None if hls is None else tuple(hls),
+                                      float(trunk_frac), float(overhead))
+    return list(order), [list(o) for o in owners], list(load)
+
+
+@functools.lru_cache(maxsize=256)
+def _split_plan(costs, world, hls, trunk_frac, overhead):
     ns = len(costs)
-    hls = hls if hls is not None else [10 ** 9] * ns
+    hls = hls if hls is not None else (10 ** 9,) * ns
     best = None
     choices = [[nb for nb in range(1, world + 1) if nb == 1 or hls[s] // nb >= MIN_BAND_ROWS] for s in range(ns)]
+    combos = 1
+    for s in sorted(range(ns), key=lambda i: (-costs[i], i)):  # band the largest scales first
+        if combos * len(choices[s]) > MAX_PLAN_COMBOS:
+            choices[s] = [1]
+        combos *= len(choices[s])
     for nbs in itertools.product(*choices):
         piece = [costs[s] * (1.0 if nbs[s] == 1 else
                              trunk_frac * min(1.0, (hls[s] / nbs[s] + 2 * BAND_MARGIN) / hls[s])
@@ -134,7 +153,7 @@ def split_plan(costs, world: int, hls=None, trunk_frac: float = TRUNK_FRAC, over
                 load[r] += piece[s]
         key = (round(max(load), 9), sum(nbs))
         if best is None or key < best[0]:
-            best = (key, order, owners, load)
+            best = (key, tuple(order), tuple(tuple(o) for o in owners), tuple(load))
     return best[1], best[2], best[3]
 
 
@@ -169,18 +188,39 @@ def band_exchange(rank_up, rank_dn, group=None):
     return ex
 
 
+def abort_band_group(body, group=None, rccl: bool = False):
+    """A band rank failed mid-frame: its neighbours are (or will be) blocked in one of the 27
+    halo exchanges.  Abort what they wait on -- the library's RCCL communicator (ncclCommAbort:
+    their pending send / recv fail) and the torch process group (gloo: the peers' pending
+    send / recv see the closed connections) -- so they raise instead of hanging until the
+    backend timeout.  The process group is unusable afterwards."""
+    if rccl:
+        try:
+            body.handle.rccl_abort()
+        except Exception:
+            pass
+        body._band_comm = None
+    try:
+        if dist.is_initialized():
+            dist.destroy_process_group(group)
+    except Exception:
+        pass
+
+
 def init_band_comm(body, group=None):
     """The library's own RCCL communicator over the ranks of `group` (Body.band_maps with
     exchange="rccl": halo send/recv on the library's stream, no Python between the layers).
     Rank 0 makes the id; it travels by one broadcast on the group.  Collective: every rank of
-    the group calls it (once per Body; later calls return at once)."""
+    the group calls it (once per Body and group: a call with the same ranks returns at once, a
+    call with another group of the same size builds a new communicator)."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    if getattr(body, "_band_comm", None) == (rank, world):
+    members = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(world))
+    if getattr(body, "_band_comm", None) == (rank, world, members):
         return
     obj = [body.handle.rccl_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
     body.handle.rccl_init(obj[0], rank, world)
-    body._band_comm = (rank, world)
+    body._band_comm = (rank, world, members)
 
 
 def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=None, split: str = "balanced",
@@ -189,12 +229,15 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
     (None elsewhere).  frame: uint8 [H,W,3] / [1,H,W,3] numpy, or a torch cuda tensor (then the
     maps stay on the device and travel over RCCL; with gloo they go through host memory).
 
-    split="scales": whole scales, longest first (scale_plan).  Result identical to
-    body.batch(frame) on one GPU: each scale's network runs with the same shapes (so the same
-    kernels and summation order) and the post path is the same code.
+    split="scales": whole scales, longest first (scale_plan).
     split="balanced" (default): split_plan, which may cut the largest scales into row bands
-    (Body.band_maps).  Where it keeps every scale whole the result is the same as "scales";
-    banded scales match the one-GPU maps to fp32 summation order (the conv grids differ).
+    (Body.band_maps).
+    Either way the result is identical to body.batch(frame) on one GPU, bit for bit: every conv
+    sums each pixel in an order fixed by the layer and the scale's geometry (k slabs, DESIGN
+    §4.1), so a band's rows and a scale on another rank equal the one-GPU network's maps, and the
+    post path is the same code.
+    A rank whose piece fails aborts the band communicator (RCCL) or the process group (gloo)
+    before re-raising, so the ranks exchanging halos with it fail instead of waiting forever.
     maps_out: a list that receives the gathered per-scale maps on `dst` (tests)."""
     import numpy as np
     dev = hasattr(frame, "data_ptr")
@@ -230,11 +273,15 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
             r0, r1 = band_rows(geoms[s][0], len(owners[s]))[b]
             up = owners[s][b - 1] if b > 0 else None
             dn = owners[s][b + 1] if b + 1 < len(owners[s]) else None
-            if on_device:  # RCCL: the library exchanges the halos itself
-                body.handle.set_band_peers(up, dn)
-                m = body.band_maps(local[0], s, r0, r1, "rccl")
-            else:
-                m = body.band_maps(local[0], s, r0, r1, band_exchange(up, dn, group))
+            try:
+                if on_device:  # RCCL: the library exchanges the halos itself
+                    body.handle.set_band_peers(up, dn)
+                    m = body.band_maps(local[0], s, r0, r1, "rccl")
+                else:
+                    m = body.band_maps(local[0], s, r0, r1, band_exchange(up, dn, group))
+            except BaseException:
+                abort_band_group(body, group, on_device)
+                raise
         pieces[(s, owners[s].index(rank))] = m if on_device else torch.from_numpy(m)
     maps = [None] * len(geoms)
     reqs = []

@@ -1,7 +1,7 @@
 """Hand() on a 368x368 crop (4 scales): host-to-host latency of one crop and of two crops
 batched (Hand.batch_crops), then per-layer kernel times of profiled passes (events around every
 launch, graphs off) of one crop and of the two-crop batch.  The engine configuration comes from
-the environment (OPOSE_LOCKSTEP, OPOSE_WIN_SK, OPOSE_SPLIT_FRAMES, ...), so an A/B is two runs
+the environment (OPOSE_LOCKSTEP, OPOSE_SPLIT_FRAMES, ...), so an A/B is two runs
 of this script."""
 import os
 import sys

@@ -98,7 +98,7 @@ class _FakeBody:
         rng = np.random.default_rng(100 + s)
         return rng.standard_normal((frame.shape[0], 57, hl, wl)).astype(np.float32)
 
-    def band_maps(self, frame, s, r0, r1, exchange=None, exact=False):
+    def band_maps(self, frame, s, r0, r1, exchange=None):
         """Rows [r0, r1) of scale_maps(s); drives the real halo exchange with a host xbuf whose
         send halves carry (scale, first row / last row) tags, and checks what comes back."""
         self.bands.append((s, r0, r1))  # (scale_maps below records s in computed)
@@ -240,7 +240,7 @@ class _FakeRcclBody(_FakeBody):
     def scale_maps(self, frame, s):
         return torch.from_numpy(super().scale_maps(frame, s))
 
-    def band_maps(self, frame, s, r0, r1, exchange=None, exact=False):
+    def band_maps(self, frame, s, r0, r1, exchange=None):
         assert exchange == "rccl" and len(self.handle.inits) == 1
         self.bands.append((s, r0, r1, self.handle.peers))
         return torch.from_numpy(_FakeBody.scale_maps(self, frame[None], s)[:, :, r0:r1].copy())
@@ -295,3 +295,65 @@ def test_balanced_split_rccl_branch_four_ranks():
     for p in procs:
         p.join(timeout=60)
     assert res == {r: True for r in range(4)}
+
+
+class _FailingBandBody(_FakeBody):
+    """Band pieces that fail on one rank after its first halo exchange (a library error, a bad
+    callback): the ranks banded with it must not wait in their remaining exchanges."""
+
+    def __init__(self, fail):
+        super().__init__()
+        self.fail = fail
+
+    def band_maps(self, frame, s, r0, r1, exchange=None):
+        if not self.fail:
+            return super().band_maps(frame, s, r0, r1, exchange)
+        xbuf = torch.zeros(4 * 64, dtype=torch.uint8)
+        exchange(xbuf, 64, 40, None)
+        raise RuntimeError("band failed on this rank")
+
+
+def _failing_worker(rank, world, port, q, bad):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from src.dist import body_scale_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=__import__("datetime").timedelta(seconds=600))
+    try:
+        body_scale_sharded(_FailingBandBody(rank == bad), np.zeros((90, 160, 3), np.uint8), rank, world, split="balanced")
+        q.put((rank, "returned"))
+    except BaseException as e:  # noqa: BLE001 -- reported to the parent
+        q.put((rank, "raised: %s" % type(e).__name__))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_failed_band_rank_does_not_hang_its_neighbours():
+    """one band rank raising mid-band used to leave its neighbours blocked in the
+    remaining halo exchanges until the backend timeout (10 min here).  body_scale_sharded now
+    aborts the group on the failing rank, so within seconds the failing rank re-raises its own
+    error, its band neighbours raise, and no rank is left waiting."""
+    import sys
+    sys.path.insert(0, PKG)
+    from src.dist import split_plan
+    world = 4
+    _, owners, _ = split_plan([g[0] * g[1] for g in GEOMS], world, [g[0] for g in GEOMS])
+    banded = [rs for rs in owners if len(rs) > 1][0]
+    bad = banded[0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29990 + os.getpid() % 8
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, q, bad)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert not p.is_alive()
+    assert res[bad] == "raised: RuntimeError", res
+    for r in banded[1:]:
+        assert res[r].startswith("raised"), res
