@@ -469,3 +469,96 @@ if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "hand368":
     install_shims()
     sys.path.insert(0, REF)
     gen_hand_planted(((604, 368, 0.85, 2),))
+
+
+# ---------------------------------------------------------------- video front end (f2)
+def gen_motion():
+    """The reference's Extract_MotionData_from_Video (srcmx/MotionEstimation.py:25-76) on fake
+    videos (oracle/glue_standins.py FakeCapture as cv2.VideoCapture): frame counts above and at
+    the decoded count, one above it (IndexError), a file that does not open; ROI crop; body and
+    bodyhand modes; the joblib file it writes, read back.  Planted Body / Hand stand-ins."""
+    import contextlib
+    import io
+    import tempfile
+    import joblib
+    install_batch_shims()
+    from oracle import glue_standins as gs
+    import cv2
+    cv2.VideoCapture = gs.FakeCapture
+    cv2.CAP_PROP_FRAME_COUNT = gs.CAP_PROP_FRAME_COUNT
+    import src.body
+    import src.hand
+    src.body.Body, src.hand.Hand = gs.StandInBody, gs.StandInHand
+    import MotionEstimation as me
+    me.body_estimation, me.hand_estimation = gs.StandInBody(), gs.StandInHand()
+    me.cv2.VideoCapture, me.cv2.CAP_PROP_FRAME_COUNT = gs.FakeCapture, gs.CAP_PROP_FRAME_COUNT
+    for seed, H, W in gs.SCENES:
+        gs.StandInBody.register(gs.frame(seed, H, W), *gs.scene(seed, H, W))
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for clip in ("clip_short.avi", "clip_exact.avi", "clip_overflow.avi", "clip_missing.avi"):
+            for mode in ("body", "bodyhand"):
+                dst = os.path.join(td, "%s-%s.pkl" % (clip, mode))
+                key = "%s_%s" % (clip.split(".")[0], mode)
+                log = io.StringIO()
+                try:
+                    with contextlib.redirect_stdout(log):
+                        ret = me.Extract_MotionData_from_Video(os.path.join(td, clip), dst, gs.ROI, mode=mode)
+                    out[key + "_ret_none"] = np.array(ret is None)
+                    out[key + "_written"] = np.array(os.path.exists(dst))
+                    if os.path.exists(dst):
+                        out[key] = joblib.load(dst)  # (written by the reference just now)
+                except IndexError:
+                    out[key + "_error"] = np.array("IndexError")
+                out[key + "_stdout"] = np.array(log.getvalue().replace(td + os.sep, ""))
+    np.savez_compressed(os.path.join(OUT, "motion_extract.npz"), **out)
+    print("wrote motion_extract.npz", {k: v.shape for k, v in out.items()})
+
+
+def gen_motion_seeded():
+    """Extract_MotionData_from_Video with the reference's own Body / Hand on the seeded networks
+    (bodyhand mode, 3 decoded frames of a 4-frame container, ROI crop): the golden the GPU
+    device ingest is held to (tests/test_gpu_pipeline.py)."""
+    import contextlib
+    import io
+    import tempfile
+    import joblib
+    install_batch_shims()
+    from oracle import glue_standins as gs
+    import cv2
+    from src.model import bodypose_model, handpose_model
+    bm = bodypose_model().eval()
+    sd = onet.seeded_state_dict("body", 0)
+    bm.load_state_dict({k: sd[".".join(k.split(".")[1:])] for k in bm.state_dict().keys()})
+    hm = handpose_model().eval()
+    sd = onet.seeded_state_dict("hand", 0)
+    hm.load_state_dict({k: sd[".".join(k.split(".")[1:])] for k in hm.state_dict().keys()})
+    body, hand = ref_body(bm), ref_hand(hm)
+    import src.body
+    import src.hand
+    src.body.Body = lambda *a, **k: body
+    src.hand.Hand = lambda *a, **k: hand
+    seeds = (910, 911, 912)
+    gs.VIDEOS["clip_seeded.avi"] = (seeds, 4)
+    cv2.VideoCapture = gs.FakeCapture
+    cv2.CAP_PROP_FRAME_COUNT = gs.CAP_PROP_FRAME_COUNT
+    import MotionEstimation as me
+    # (the module may already be imported by gen_motion with the stand-ins)
+    me.body_estimation, me.hand_estimation = body, hand
+    me.cv2.VideoCapture, me.cv2.CAP_PROP_FRAME_COUNT = gs.FakeCapture, gs.CAP_PROP_FRAME_COUNT
+    with tempfile.TemporaryDirectory() as td:
+        dst = os.path.join(td, "seeded.pkl")
+        with contextlib.redirect_stdout(io.StringIO()):
+            me.Extract_MotionData_from_Video(os.path.join(td, "clip_seeded.avi"), dst, gs.ROI, mode="bodyhand")
+        motion = joblib.load(dst)
+    np.savez_compressed(os.path.join(OUT, "motion_extract_seeded.npz"), seeds=np.array(seeds), count=np.array(4),
+                        motion=motion)
+    print("wrote motion_extract_seeded.npz", motion.shape, (motion != 0).any(2).sum(1))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "motion":
+    sys.path.insert(0, REF)
+    sys.path.insert(0, os.path.join(REF, "srcmx"))
+    torch.set_num_threads(8)
+    gen_motion_seeded()  # (first: gen_motion replaces src.body.Body / src.hand.Hand by stand-ins)
+    gen_motion()

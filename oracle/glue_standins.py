@@ -124,3 +124,47 @@ class StandInHand:
 
     def batch_crops(self, crops):
         return [self(c) for c in crops]
+
+
+# ---------------------------------------------------------------- video front end
+# Extract_MotionData_from_Video (srcmx/MotionEstimation.py:25-76) reads cv2.VideoCapture: the
+# frame count the container reports sizes MotionMat, the frames that decode fill it.
+CAP_PROP_FRAME_COUNT = 7  # cv2.CAP_PROP_FRAME_COUNT
+ROI = [(40, 30), (360, 270)]  # Recpoint [(x0, y0), (x1, y1)]: a 240 x 320 crop of 300 x 400 frames
+
+
+def video_frame(seed):
+    """A 300 x 400 frame whose ROI crop is frame(seed, 240, 320) (a registered scene)."""
+    full = np.random.default_rng(seed + 7).integers(0, 256, (300, 400, 3), dtype=np.uint8)
+    full[ROI[0][1]:ROI[1][1], ROI[0][0]:ROI[1][0]] = frame(seed, 240, 320)
+    return full
+
+
+# path -> (seeds of the frames that decode, the count the container reports)
+VIDEOS = {
+    "clip_short.avi": ((900, 901, 902, 903, 904), 7),     # two frames fewer than reported: zero rows
+    "clip_exact.avi": ((903, 900, 904), 3),
+    "clip_overflow.avi": ((900, 901, 902, 903, 904), 3),  # more than reported: IndexError
+}
+
+
+class FakeCapture:
+    """cv2.VideoCapture stand-in over VIDEOS (a path not in it does not open)."""
+
+    def __init__(self, path):
+        import os
+        self.v = VIDEOS.get(os.path.basename(path))
+        self.i = 0
+
+    def isOpened(self):
+        return self.v is not None
+
+    def get(self, prop):
+        assert prop == CAP_PROP_FRAME_COUNT
+        return float(self.v[1])
+
+    def read(self):
+        if self.v is None or self.i >= len(self.v[0]):
+            return False, None
+        self.i += 1
+        return True, video_frame(self.v[0][self.i - 1])

@@ -855,6 +855,9 @@ static XAct frame_view(const XAct& a, int n, int H, int W) {
 //    one segment per frame (frame views of the same buffers; a crop batch's 92 x 92 scale);
 //  * body layers of fewer than 4096 pixels (C2's single frame, a pyramid's 0.5 scale): conv_x6,
 //    whose 128 x 64 tiles spread a small layer over the chip;
+//  * the hand's 512-channel 3x3 layers at H/8 (conv4_x, conv5_x): conv_x6, whose 256 x 128 tiles
+//    cover a 368 crop's 4-scale pyramid in one data-parallel round (254 tiles; the window
+//    kernel's 128 x 256 tiles make 260: 225 vs 270 TF/s);
 //  * everything else (dense inputs, pooled convs, 1x1): conv_x6.
 enum { kKernelX6 = 0, kKernelWin = 1, kKernelWinFrames = 2 };
 static int seg_kernel(const opose_ctx* h, const ConvSeg& sg, bool pool) {
@@ -862,6 +865,7 @@ static int seg_kernel(const opose_ctx* h, const ConvSeg& sg, bool pool) {
     if (!h->win7 || pool || !c->wx6p || !sg.in.padded || (c->ks != 3 && c->ks != 7)) return kKernelX6;
     const long lpix = (long)sg.N * (sg.Hl ? sg.Hl : sg.H) * sg.W;
     if (c->net == OPOSE_NET_BODY && lpix < 4096) return kKernelX6;
+    if (c->net == OPOSE_NET_HAND && c->ks == 3 && c->lvl == 3) return kKernelX6;
     if (sg.N == 1) return conv_win_fits_rows(sg.W, c->ks) ? kKernelWin : kKernelX6;
     if (conv_win_fits(sg.N, sg.H, sg.W, c->ks)) return kKernelWin;
     if (c->ks == 7 && h->split_frames && conv_win_fits_rows(sg.W, c->ks)) return kKernelWinFrames;
@@ -873,20 +877,21 @@ static int seg_kernel(const opose_ctx* h, const ConvSeg& sg, bool pool) {
 // grid, its other groups or a row band's rows.  Large layers keep one slab (one run over all
 // chunks, the data-parallel grids of the bench's 32-frame batch); smaller ones are cut so that
 // their work units fill the chip, counting tiles of the kernel's smallest tile (window: 128 x 256,
-// conv_x6: 128 x 64) and both branches of a CPM pair.  The hand's 7x7 / 3x3 layers run as one
-// launch per layer for a 4-scale pyramid (lockstep): their counts are set per scale size so that
-// the pyramid's units pack evenly over 256 workgroups (longest-first, lpt_units).
+// conv_x6: 128 x 64) and both branches of a CPM pair.  The hand's layers run as one launch per
+// layer for a 4-scale pyramid (lockstep): its 3x3 layers fill the chip with whole tiles (254 /
+// 502 tiles over the pyramid), and the 7x7 counts are set per scale size so that the pyramid's
+// units pack evenly over 256 workgroups (longest-first, lpt_units).
 static int slab_count(const DevConv* c, bool win, int N, int H, int W, bool pool) {
     const int nK = win ? c->nK6p : c->nK6;
-    if (pool || nK < 8) return 1;
+    if (pool || c->ks == 1 || nK < 8) return 1;  // 1x1: the closing pairs' unfused form sums like the fused chain
     const int smax = nK / 4;
     const long npix = (long)N * H * W;
     const double mr = c->Mpad / 128.0;
     auto clampS = [&](long s) { return (int)std::max<long>(1, std::min<long>(s, smax)); };
-    if (c->net == OPOSE_NET_HAND && win) {
+    if (c->net == OPOSE_NET_HAND) {
+        if (c->ks != 7 || !win) return 1;
         const double T = std::ceil(npix / 256.0) * mr;
-        if (c->ks == 7) return clampS(T < 6 ? 16 : T < 12 ? 12 : T < 30 ? 8 : T < 60 ? 7 : T < 120 ? 4 : T < 240 ? 2 : 1);
-        return clampS(T < 12 ? 12 : T < 30 ? 6 : T < 60 ? 4 : T < 120 ? 2 : 1);
+        return clampS(T < 6 ? 16 : T < 12 ? 12 : T < 30 ? 8 : T < 60 ? 7 : T < 120 ? 4 : T < 240 ? 2 : 1);
     }
     const int mult = c->pair ? 2 : 1;
     if (win) {
@@ -964,6 +969,7 @@ static opose_ctx::ConvPlan plan_launch(opose_ctx* h, const std::vector<ConvSeg>&
         h->sched_host.push_back(std::move(flat));
         const std::vector<int>& src = h->sched_host.back();
         OPOSE_HIP_CHECK(hipMemcpyAsync(d, src.data(), src.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+        OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));  // (once per launch signature)
         h->sched_mem.push_back(d);
         best.sched = d;
     }

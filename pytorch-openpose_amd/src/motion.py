@@ -12,7 +12,13 @@ Frames are processed in batches (one Body launch sequence per batch, all hands o
 one crop-batched Hand pass) instead of one frame at a time; per-frame results are those of
 `src.pipeline.motion_data_every_frame`.  Any iterable of uint8 BGR frames works as a source;
 `VideoFrames` reads a video file through OpenCV when it is installed (it is not part of this
-image: decode elsewhere and pass the frames).
+image: decode elsewhere and pass the frames, or pass any cv2.VideoCapture-like `capture`).
+
+Like the reference, the matrix has one row per frame the container *reports*
+(CAP_PROP_FRAME_COUNT, srcmx/MotionEstimation.py:45-50): rows of frames that never decode stay
+zero, a video that decodes more frames than it reports raises IndexError, and a video that does
+not open is reported and yields None (`Extract_MotionData_from_Video`, the reference's entry
+point, :25-76).
 
 Ingest (the reference's DataLoader over decoded frames, srcmx/Batch_model.py:36-52, 409-412, into
 the per-video loop of srcmx/MotionEstimation.py:61-76): with a GPU, `extract_motion_data` streams
@@ -29,26 +35,33 @@ import numpy as np
 
 
 
-class VideoFrames(object):
-    """Sequential BGR frames of a video file, optionally cropped (VideoDataset semantics)."""
+CAP_PROP_FRAME_COUNT = 7  # cv2.CAP_PROP_FRAME_COUNT
 
-    def __init__(self, videopath, crop=None):
-        try:
-            import cv2
-        except ImportError as e:  # pragma: no cover - cv2 is absent in this image
-            raise ImportError("VideoFrames needs OpenCV (cv2) to decode video; pass decoded frames "
-                              "to extract_motion_data instead") from e
-        self._cv2 = cv2
-        self.video = cv2.VideoCapture(videopath)
-        if not self.video.isOpened():
-            raise FileNotFoundError(videopath)
+
+class VideoFrames(object):
+    """Sequential BGR frames of a video file, optionally cropped (VideoDataset semantics).
+
+    capture: a cv2.VideoCapture-like factory (isOpened / get(CAP_PROP_FRAME_COUNT) / read);
+    default cv2.VideoCapture.  len() is the count the container reports; `opened` is False for a
+    file that does not open (then it has no frames)."""
+
+    def __init__(self, videopath, crop=None, capture=None):
+        if capture is None:
+            try:
+                import cv2
+            except ImportError as e:  # pragma: no cover - cv2 is absent in this image
+                raise ImportError("VideoFrames needs OpenCV (cv2) to decode video; pass decoded frames "
+                                  "to extract_motion_data instead, or a capture factory") from e
+            capture = cv2.VideoCapture
+        self.video = capture(videopath)
+        self.opened = bool(self.video.isOpened())
         self.crop = crop
 
     def __len__(self):
-        return int(self.video.get(self._cv2.CAP_PROP_FRAME_COUNT))
+        return int(self.video.get(CAP_PROP_FRAME_COUNT)) if self.opened else 0
 
     def __iter__(self):
-        while True:
+        while self.opened:
             ok, image = self.video.read()
             if not ok:
                 return
@@ -150,11 +163,17 @@ def _device_poses(frames, body, hand, recpoint, mode, batch):
     return out
 
 
-def extract_motion_data(frames, body, hand=None, outpath=None, recpoint=None, mode="body", batch=32, device=None):
-    """MotionMat [n_frames, 18 | 60, 3] for an iterable of uint8 BGR frames (equal sizes after
-    cropping).  mode "body" (18 joints) or "bodyhand" (needs `hand`); saved with joblib.dump
-    when `outpath` is given, like Extract_MotionData_from_Video.  device=None: the pinned,
-    double-buffered GPU ingest when torch sees a GPU, else host batches (Body.batch)."""
+def extract_motion_data(frames, body, hand=None, outpath=None, recpoint=None, mode="body", batch=32, device=None,
+                        count=None):
+    """MotionMat [count, 18 | 60, 3] float64 for an iterable of uint8 BGR frames (equal sizes
+    after cropping).  mode "body" (18 joints) or "bodyhand" (needs `hand`); saved with
+    joblib.dump when `outpath` is given, like Extract_MotionData_from_Video.  device=None: the
+    pinned, double-buffered GPU ingest when torch sees a GPU, else host batches (Body.batch).
+
+    count: rows of the matrix, the frame count the source reports (default len(frames) when it
+    has one -- a VideoFrames' CAP_PROP_FRAME_COUNT -- else the frames decoded).  Frames past the
+    decoded ones stay zero rows; more decoded frames than `count` raise IndexError, as the
+    reference's preallocated MotionMat does (srcmx/MotionEstimation.py:45-50, 72-73)."""
     if mode not in ("body", "bodyhand"):
         raise ValueError("mode must be 'body' or 'bodyhand'")
     if mode == "bodyhand" and hand is None:
@@ -165,10 +184,47 @@ def extract_motion_data(frames, body, hand=None, outpath=None, recpoint=None, mo
             device = torch.cuda.is_available()
         except ImportError:
             device = False
+    if count is None and hasattr(frames, "__len__"):
+        count = len(frames)
     out = (_device_poses if device else _host_poses)(frames, body, hand, recpoint, mode, batch)
     joints = 60 if mode == "bodyhand" else 18
-    motion = np.concatenate(out) if out else np.zeros((0, joints, 3))
+    poses = np.concatenate(out) if out else np.zeros((0, joints, 3))
+    if count is None:
+        count = len(poses)
+    if len(poses) > count:
+        raise IndexError("index %d is out of bounds for axis 0 with size %d" % (count, count))
+    motion = np.zeros((count, joints, 3))
+    motion[:len(poses)] = poses
     if outpath is not None:
         import joblib
         joblib.dump(motion, outpath)
     return motion
+
+
+def Extract_MotionData_from_Video(videopath, outpath, Recpoint, mode="body", overwrite=False, *, body, hand=None,
+                                  batch=32, device=None, capture=None):
+    """The reference's entry point (srcmx/MotionEstimation.py:25-76) on the GPU Body / Hand:
+    the video's frames cropped to Recpoint [(x0, y0), (x1, y1)], MotionMat [count, 18 | 60, 3]
+    (count = CAP_PROP_FRAME_COUNT; frames that do not decode leave zero rows) written to
+    `outpath` with joblib.dump.  Returns None, like the reference (the matrix is the file); a
+    video that does not open is reported on stdout and nothing is written.  `overwrite` is
+    unused, as in the reference.  body / hand: the estimators (the reference's module-level
+    body_estimation / hand_estimation); capture: see VideoFrames."""
+    import os
+    del overwrite
+    video = VideoFrames(videopath, crop=Recpoint, capture=capture)
+    if not video.opened:
+        print('the file %s is not exist' % videopath)
+        return None
+    count = len(video)
+    outname = os.path.split(outpath)[1]
+
+    def progress():
+        for index, frame in enumerate(video):
+            if index % 100 == 0:
+                print('%s-%d/%d' % (outname, index, count))
+            yield frame
+
+    extract_motion_data(progress(), body, hand, outpath=outpath, mode=mode, batch=batch, device=device, count=count)
+    print('%s is saved!' % outpath)
+    return None

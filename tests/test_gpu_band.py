@@ -32,7 +32,7 @@ def bodies():
     from src.body import Body
     from src.weights import seeded_state_dict
     sd = seeded_state_dict("body", 0)
-    return [Body(sd, scale_search=SCALES) for _ in range(3)]
+    return [Body(sd, scale_search=SCALES) for _ in range(5)]
 
 
 @pytest.fixture(scope="module")

@@ -147,3 +147,35 @@ def test_hand_batch_crops_beyond_one_launch(nets):
     assert len(batch) == 12
     for c, b in zip(crops, batch):
         np.testing.assert_allclose(b, hand(c), rtol=1e-4, atol=1e-5)
+
+
+def test_extract_motion_video_device_ingest_matches_reference(nets, tmp_path):
+    """f2 end to end against the reference's own Extract_MotionData_from_Video
+    (srcmx/MotionEstimation.py:25-76) run with its Body / Hand on the seeded networks
+    (tests/golden/motion_extract_seeded.npz, oracle/gen_golden.py motion): a fake container that
+    reports 4 frames and decodes 3 (the last row stays zero), the ROI crop, bodyhand mode (a
+    flipped left hand on frame 2), read through src.motion's pinned double-buffered device ingest
+    in batches of 2 and written with joblib.  Bar: the north-star one -- every joint's pixel
+    identical, scores within fp32 network noise (rtol 1e-3)."""
+    import contextlib
+    import io
+    import os
+
+    import joblib
+
+    from conftest import GOLDEN
+    from oracle import glue_standins as gs
+    from src.motion import Extract_MotionData_from_Video
+    bsd, hsd, Body, Hand = nets
+    g = np.load(os.path.join(GOLDEN, "motion_extract_seeded.npz"))
+    gs.VIDEOS["clip_seeded.avi"] = (tuple(int(s) for s in g["seeds"]), int(g["count"]))
+    dst = os.path.join(str(tmp_path), "seeded.pkl")
+    with contextlib.redirect_stdout(io.StringIO()):
+        assert Extract_MotionData_from_Video(os.path.join(str(tmp_path), "clip_seeded.avi"), dst, gs.ROI,
+                                             mode="bodyhand", body=Body(bsd), hand=Hand(hsd), batch=2,
+                                             device=True, capture=gs.FakeCapture) is None
+    got, exp = joblib.load(dst), g["motion"]
+    assert got.shape == exp.shape == (4, 60, 3) and got.dtype == exp.dtype
+    assert (exp[2, 18:39] != 0).any() and not exp[3].any()
+    assert np.array_equal(got[..., :2], exp[..., :2])
+    np.testing.assert_allclose(got[..., 2], exp[..., 2], rtol=1e-3, atol=1e-6)
