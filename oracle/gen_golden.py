@@ -562,3 +562,41 @@ if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "motion":
     torch.set_num_threads(8)
     gen_motion_seeded()  # (first: gen_motion replaces src.body.Body / src.hand.Hand by stand-ins)
     gen_motion()
+
+
+# ---------------------------------------------------------------- full-size C3 / C5 (verdict r3 item 2)
+def gen_fullsize():
+    """Body() on one 1080x1920 frame with scale_search [0.5, 1, 1.5, 2] (C5, the C5 calibration)
+    and Hand() on one 368x368 crop (C3's four pyramid networks 184^2 .. 736^2), through the oracle
+    (oracle/network.py + oracle/body_post.py / hand_post.py, pinned to the reference's goldens by
+    tests/test_oracle_golden.py) in float32 -- the reference's arithmetic -- and in float64 (the
+    exact answer near ties).  The GPU tests regenerate the inputs from the seeds; only the outputs
+    are stored (tests/golden/fullsize_c3_c5.npz)."""
+    sys.path.insert(0, os.path.join(REPO, "pytorch-openpose_amd"))
+    from oracle import body_post, hand_post
+    from src.weights import c5_out_scale
+    torch.set_num_threads(8)
+    out = {}
+    img = np.random.default_rng(53).integers(0, 256, (1080, 1920, 3), dtype=np.uint8)
+    sd = onet.seeded_state_dict("body", 0, out_scale=c5_out_scale())
+    for tag, d, dbl in (("f32", sd, False), ("f64", {k: v.double() for k, v in sd.items()}, True)):
+        def fn(x, d=d, dbl=dbl):
+            xx = torch.from_numpy(x)
+            p, h = onet.body_forward(xx.double() if dbl else xx, d)
+            return p.float().numpy(), h.float().numpy()
+        c, s = body_post.body_infer(img, fn, scale_search=(0.5, 1.0, 1.5, 2.0))
+        out["c5_cand_" + tag], out["c5_subset_" + tag] = np.asarray(c, np.float64), s
+        print("C5", tag, np.shape(c), s.shape)
+    crop = np.random.default_rng(54).integers(0, 256, (368, 368, 3), dtype=np.uint8)
+    hsd = onet.seeded_state_dict("hand", 0)
+    for tag, d, dbl in (("f32", hsd, False), ("f64", {k: v.double() for k, v in hsd.items()}, True)):
+        def hfn(x, d=d, dbl=dbl):
+            xx = torch.from_numpy(x)
+            return onet.hand_forward(xx.double() if dbl else xx, d).float().numpy()
+        out["c3_peaks_" + tag] = hand_post.hand_infer(crop, hfn)
+        print("C3", tag, out["c3_peaks_" + tag][:3])
+    np.savez_compressed(os.path.join(OUT, "fullsize_c3_c5.npz"), c5_seed=np.array(53), c3_seed=np.array(54), **out)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "fullsize":
+    gen_fullsize()

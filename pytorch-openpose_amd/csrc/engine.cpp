@@ -8,6 +8,9 @@
 // CPM branches of a stage share one launch (combined M for their common first conv,
 // two GEMM groups for the rest); stage concatenation is implicit (channel-slice writes).
 #include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -271,6 +274,7 @@ struct opose_ctx {
         int* sched = nullptr;
     };
     std::map<std::string, ConvPlan> plans;
+    std::map<std::string, int> slab_cache;  // engine slab_count
     std::vector<int*> sched_mem;
     std::vector<std::vector<int>> sched_host;  // sources of the asynchronous uploads
     DevBuf frames, mids[2][kMaxScales], avg, cnt, list, peak_pos, part_cnt, score, conn, conn_cnt, records, maps_in,
@@ -290,11 +294,10 @@ struct opose_ctx {
         const char* e = getenv("OPOSE_SCALE_STREAMS");
         return !(e && e[0] == '0');
     }();
-    // split-bf16 path: the scales' networks in lockstep, one conv launch per layer for all of them
-    // (Hand: default; OPOSE_LOCKSTEP=0: one network per scale, concurrent streams when
-    // scale_streams).  Body pyramids: OPOSE_LOCKSTEP=2 -- by default they keep one network per
-    // scale, so that the scale-sharded C5 split (opose_body_scale_maps per rank) reproduces
-    // Body(frame) bit for bit: a lockstep launch's stream-K plan depends on every scale.
+    // split-bf16 path: a pyramid's networks (Hand()'s four scales, a multi-scale Body's) in
+    // lockstep, one conv launch per layer for all of them (default); OPOSE_LOCKSTEP=0: one network
+    // per scale, concurrent streams when scale_streams (the reference of the lockstep tests; the
+    // same outputs bit for bit: a pixel's summation order does not depend on the launch).
     int lockstep = [] {
         const char* e = getenv("OPOSE_LOCKSTEP");
         return e ? std::atoi(e) : 1;
@@ -380,21 +383,22 @@ struct opose_ctx {
     int band_up = -1, band_dn = -1;
     ~opose_ctx();
     void release() {
-        if (nstream) {
-            (void)hipStreamSynchronize(nstream);
-            (void)hipStreamDestroy(nstream);
-        }
+        // drain every stream first, then the graph executables (they may reference the scale
+        // streams' captured work), then streams, events and memory
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (nstream) (void)hipStreamSynchronize(nstream);
+        for (int i = 0; i < kMaxScales; ++i)
+            if (sstream[i]) (void)hipStreamSynchronize(sstream[i]);
+        for (auto& kv : graphs)
+            if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+        graphs.clear();
+        if (nstream) (void)hipStreamDestroy(nstream);
         for (hipEvent_t e : {ev_net, ev_main, ev_post[0], ev_post[1], ev_ext, ev_sig, ev_fork})
             if (e) (void)hipEventDestroy(e);
         for (int i = 0; i < kMaxScales; ++i) {
-            if (sstream[i]) {
-                (void)hipStreamSynchronize(sstream[i]);
-                (void)hipStreamDestroy(sstream[i]);
-            }
+            if (sstream[i]) (void)hipStreamDestroy(sstream[i]);
             if (ev_join[i]) (void)hipEventDestroy(ev_join[i]);
         }
-        for (auto& kv : graphs)
-            if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
         for (int* p : sched_mem) (void)hipFree(p);
         for (auto e : event_pool) (void)hipEventDestroy(e);
         if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -872,68 +876,40 @@ static int seg_kernel(const opose_ctx* h, const ConvSeg& sg, bool pool) {
     return kKernelX6;
 }
 
-// k slabs of a segment (common.h X6Group::slabs): a function of the layer, its kernel family and
-// the segment's logical geometry (N frames of H x W) -- never of the launch that runs it, its
-// grid, its other groups or a row band's rows.  Large layers keep one slab (one run over all
-// chunks, the data-parallel grids of the bench's 32-frame batch); smaller ones are cut so that
-// their work units fill the chip, counting tiles of the kernel's smallest tile (window: 128 x 256,
-// conv_x6: 128 x 64) and both branches of a CPM pair.  The hand's layers run as one launch per
-// layer for a 4-scale pyramid (lockstep): its 3x3 layers fill the chip with whole tiles (254 /
-// 502 tiles over the pyramid), and the 7x7 counts are set per scale size so that the pyramid's
-// units pack evenly over 256 workgroups (longest-first, lpt_units).
-static int slab_count(const DevConv* c, bool win, int N, int H, int W, bool pool) {
-    const int nK = win ? c->nK6p : c->nK6;
-    if (pool || c->ks == 1 || nK < 8) return 1;  // 1x1: the closing pairs' unfused form sums like the fused chain
-    const int smax = nK / 4;
-    const long npix = (long)N * H * W;
-    const double mr = c->Mpad / 128.0;
-    auto clampS = [&](long s) { return (int)std::max<long>(1, std::min<long>(s, smax)); };
-    if (c->net == OPOSE_NET_HAND) {
-        if (c->ks != 7 || !win) return 1;
-        const double T = std::ceil(npix / 256.0) * mr;
-        return clampS(T < 6 ? 16 : T < 12 ? 12 : T < 30 ? 8 : T < 60 ? 7 : T < 120 ? 4 : T < 240 ? 2 : 1);
-    }
-    const int mult = c->pair ? 2 : 1;
-    if (win) {
-        const double T = std::ceil(npix / 256.0) * mr * mult;
-        return T >= 160 ? 1 : clampS(std::max(2L, std::lround(320.0 / T)));
-    }
-    const double T = std::ceil(npix / 64.0) * mr * mult;
-    return T >= 640 ? 1 : clampS(std::max(2L, std::lround(384.0 / T)));
-}
-
 // conv_x6 tile configurations: mt, pt, co-resident workgroups per CU, cost per chunk relative to
 // a 64 x 64 tile's (measured, scripts/conv_timing.py; rounds 1-2)
 static const int kX6Cfg[6][3] = {{128, 128, 1}, {128, 256, 1}, {256, 128, 1}, {128, 64, 2}, {64, 128, 2}, {64, 64, 3}};
 static const double kX6Ovh[6] = {1.5, 1.0, 0.96, 1.1, 1.1, 1.2};
 
-// Launch plan of one kernel family over segments whose slab counts are set: tile shape, grid,
-// and (units > grid or unequal units) the longest-first unit schedule.  Cached per signature.
-static opose_ctx::ConvPlan plan_launch(opose_ctx* h, const std::vector<ConvSeg>& segs, bool win, bool pool, int nK,
-                                       int Mpad) {
-    std::string key = (win ? "w" : "x") + std::to_string(pool) + "/" + std::to_string(nK) + "/" + std::to_string(Mpad);
-    for (const ConvSeg& s : segs)
-        key += "/" + std::to_string((long)s.N * s.H * s.W) + ":" + std::to_string(s.slabs) + ":" +
-               std::to_string(pool ? s.W : 0);
-    auto it = h->plans.find(key);
-    if (it != h->plans.end()) return it->second;
-    auto groups_for = [&](int mt, int pt) {
-        std::vector<SlabGroup> gs;
-        for (const ConvSeg& s : segs) {
-            const long np = pool ? (long)s.N * (s.H / 2) * (s.W / 2) * 4 : (long)s.N * s.H * s.W;
-            gs.push_back({(long)(Mpad / mt) * ((np + pt - 1) / pt), s.slabs});
-        }
-        return gs;
-    };
+// GEMM columns and slab count of one group of a launch
+struct ColGroup {
+    long cols;
+    int S;
+};
+
+static std::vector<SlabGroup> slab_groups(const std::vector<ColGroup>& cg, int Mpad, int mt, int pt) {
+    std::vector<SlabGroup> gs;
+    for (const ColGroup& c : cg) gs.push_back({(long)(Mpad / mt) * ((c.cols + pt - 1) / pt), c.S});
+    return gs;
+}
+
+// Tile shape and grid of one launch (window kernel: 128 x 256 only) priced in choose_tile's units
+// (a 32-deep chunk of a 64 x 64 tile = 0.4): the largest workgroup load (one-slab launches: rounds
+// of whole tiles over the hardware dispatcher; else the longest-first unit schedule) times the
+// tile's chunk cost, plus the slab partials' HBM round trip and the fixup launch.
+struct TilePick {
+    int mt = 0, pt = 0, grid = 0;
+    double cost = 1e300;
+};
+static TilePick pick_tile(const std::vector<ColGroup>& cg, bool win, int nK, int Mpad) {
     bool multi = false;
-    for (const ConvSeg& s : segs) multi = multi || s.slabs > 1;
-    opose_ctx::ConvPlan best;
-    double best_cost = 1e300;
+    for (const ColGroup& c : cg) multi = multi || c.S > 1;
+    TilePick best;
     for (int ci = 0; ci < 6; ++ci) {
         const int mt = win ? 128 : kX6Cfg[ci][0], pt = win ? 256 : kX6Cfg[ci][1], occ = win ? 1 : kX6Cfg[ci][2];
         if (win && ci > 0) break;
         if (Mpad % mt) continue;
-        const std::vector<SlabGroup> gs = groups_for(mt, pt);
+        const std::vector<SlabGroup> gs = slab_groups(cg, Mpad, mt, pt);
         long units = 0, tiles = 0;
         for (const SlabGroup& g : gs) {
             units += g.tiles * g.S;
@@ -947,20 +923,97 @@ static opose_ctx::ConvPlan plan_launch(opose_ctx* h, const std::vector<ConvSeg>&
         const double share = G <= 256 ? (occ >= 2 ? 1.6 : 1.0) : (multi ? std::min<double>(occ, (double)G / 256.0) : occ);
         double cost = mk * unit * share;
         if (multi) cost += (double)units * mt * pt * 4.0 * 2.0 / 5e12 / 0.42e-6 + 8.0;  // slab partials + fixup
-        if (cost < best_cost * 0.97) {
-            best_cost = cost;
+        if (cost < best.cost * 0.97) {
+            best.cost = cost;
             best.mt = mt;
             best.pt = pt;
             best.grid = (int)G;
         }
     }
+    return best;
+}
+
+// k slabs of a segment (common.h X6Group::slabs): a function of the layer, its kernel family and
+// the segment's logical geometry (N frames of H x W) -- never of the launch that runs it, its
+// grid, its other groups or a row band's rows.  Large layers keep one slab (one run over all
+// chunks, the data-parallel grids of the bench's 32-frame batch); smaller ones are cut so that
+// their work units fill the chip, counting tiles of the kernel's smallest tile (window: 128 x 256,
+// conv_x6: 128 x 64) and both branches of a CPM pair.  The hand's layers run as one launch per
+// layer for a 4-scale pyramid (lockstep): its 3x3 layers fill the chip with whole tiles (254 /
+// 502 tiles over the pyramid), and the 7x7 counts are set per scale size so that the pyramid's
+// units pack evenly over 256 workgroups (longest-first, lpt_units).
+static int slab_count(opose_ctx* h, const DevConv* c, bool win, int N, int H, int W, bool pool) {
+    const int nK = win ? c->nK6p : c->nK6;
+    if (pool || c->ks == 1 || nK < 8) return 1;  // 1x1: the closing pairs' unfused form sums like the fused chain
+    const int smax = nK / 4;
+    const long npix = (long)N * H * W;
+    const double mr = c->Mpad / 128.0;
+    auto clampS = [&](long s) { return (int)std::max<long>(1, std::min<long>(s, smax)); };
+    if (c->net == OPOSE_NET_HAND) {
+        if (c->ks != 7 || !win) return 1;
+        const double T = std::ceil(npix / 256.0) * mr;
+        return clampS(T < 6 ? 16 : T < 12 ? 12 : T < 30 ? 8 : T < 60 ? 7 : T < 120 ? 4 : T < 240 ? 2 : 1);
+    }
+    const int mult = c->pair ? 2 : 1;
+    if (std::ceil(npix / 256.0) * mr * mult >= 160) return 1;  // the bench's batches: whole tiles fill the chip
+    // otherwise the count that prices lowest for the segment run alone (with its CPM sibling), as
+    // Body(frame) runs a scale -- plus, for one frame whose H/8 map has >= 40 rows (a scale the
+    // balanced C5 split may cut into row bands, src/dist.py split_plan), the same layer on a fifth
+    // of the rows (+ the band trunk's margin), as a band rank runs it.  A band's smaller launch
+    // may take smaller tiles: the tile does not change a pixel's sum, the slab count does.
+    const int h8 = H >> (3 - std::min(3, c->lvl));
+    const long bpix = N == 1 && h8 >= 40
+                          ? (long)std::min(H, H / 5 + (c->lvl < 3 ? 20 << (3 - c->lvl) : 0)) * W
+                          : 0;
+    const std::string key = std::to_string(win) + "/" + std::to_string(nK) + "/" + std::to_string(c->Mpad) + "/" +
+                            std::to_string(npix) + "/" + std::to_string(mult) + "/" + std::to_string(bpix);
+    auto it = h->slab_cache.find(key);
+    if (it != h->slab_cache.end()) return it->second;
+    static const int cand[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 28, 32, 40, 48, 64};
+    int best = 1;
+    double best_cost = 1e300;
+    for (int S : cand) {
+        if (S > std::max(1, smax)) break;
+        double cost = pick_tile(std::vector<ColGroup>(mult, ColGroup{npix, S}), win, nK, c->Mpad).cost;
+        if (bpix) cost += pick_tile(std::vector<ColGroup>(mult, ColGroup{bpix, S}), win, nK, c->Mpad).cost;
+        if (cost < best_cost * 0.97) {
+            best_cost = cost;
+            best = S;
+        }
+    }
+    h->slab_cache[key] = best;
+    return best;
+}
+
+// Launch plan of one kernel family over segments whose slab counts are set: tile shape, grid,
+// and (multi-slab launches) the longest-first unit schedule.  Cached per signature.
+static opose_ctx::ConvPlan plan_launch(opose_ctx* h, const std::vector<ConvSeg>& segs, bool win, bool pool, int nK,
+                                       int Mpad) {
+    std::string key = (win ? "w" : "x") + std::to_string(pool) + "/" + std::to_string(nK) + "/" + std::to_string(Mpad);
+    for (const ConvSeg& s : segs)
+        key += "/" + std::to_string((long)s.N * s.H * s.W) + ":" + std::to_string(s.slabs) + ":" +
+               std::to_string(pool ? s.W : 0);
+    auto it = h->plans.find(key);
+    if (it != h->plans.end()) return it->second;
+    std::vector<ColGroup> cg;
+    bool multi = false;
+    for (const ConvSeg& s : segs) {
+        cg.push_back({pool ? (long)s.N * (s.H / 2) * (s.W / 2) * 4 : (long)s.N * s.H * s.W, s.slabs});
+        multi = multi || s.slabs > 1;
+    }
+    const TilePick tp = pick_tile(cg, win, nK, Mpad);
+    opose_ctx::ConvPlan best;
+    best.mt = tp.mt;
+    best.pt = tp.pt;
+    best.grid = tp.grid;
     best.sched = nullptr;
     if (multi) {
         std::vector<std::vector<int>> lists;
-        lpt_units(groups_for(best.mt, best.pt), nK, best.grid, &lists);
+        lpt_units(slab_groups(cg, Mpad, best.mt, best.pt), nK, best.grid, &lists);
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         OPOSE_HIP_CHECK(hipStreamIsCapturing(h->stream, &cs));
         if (cs != hipStreamCaptureStatusNone) return best;  // (captured: contiguous unit ranges, same sums)
+        if (getenv("OPOSE_NO_SCHED")) { h->plans[key] = best; return best; }  // TEMP diag
         std::vector<int> flat(best.grid + 1, 0);
         for (int w = 0; w < best.grid; ++w) flat[w + 1] = flat[w] + (int)lists[w].size();
         for (const auto& L : lists) flat.insert(flat.end(), L.begin(), L.end());
@@ -1054,7 +1107,7 @@ static void run_conv_x6_segs(opose_ctx* h, const std::vector<ConvSeg>& segs, boo
         ConvSeg sg = s0;
         const int kind = seg_kernel(h, sg, pool);
         const bool win = kind != kKernelX6;
-        if (!sg.slabs) sg.slabs = slab_count(sg.c, win, sg.N, sg.Hl ? sg.Hl : sg.H, sg.W, pool);
+        if (!sg.slabs) sg.slabs = slab_count(h, sg.c, win, sg.N, sg.Hl ? sg.Hl : sg.H, sg.W, pool);
         if (kind == kKernelWinFrames) {
             for (int n = 0; n < sg.N; ++n) {
                 ConvSeg f = sg;
@@ -2021,7 +2074,15 @@ void opose_default_params(int net, opose_params* p) {
     p->thre_hand = 0.03;
 }
 
+static void segv_trace(int sig) {
+    void* bt[64];
+    const int n = backtrace(bt, 64);
+    backtrace_symbols_fd(bt, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
 int opose_create(int device, opose_t** out) {
+    if (getenv("OPOSE_SEGV_TRACE")) signal(SIGSEGV, segv_trace);
     if (!out) return OPOSE_E_ARG;
     *out = nullptr;
     auto* h = new opose_ctx();
@@ -2386,7 +2447,7 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
             float* S = body_net(h, x, N, g.Hp, g.Wp);
             upsample_to_mid(h, s, S, 185, N, g, 56);
         };
-        const bool lockstep = h->x6 && h->lockstep == 2 && p.n_scales > 1;
+        const bool lockstep = h->x6 && h->lockstep && p.n_scales > 1;
         auto net_part = [&] {
             if (lockstep)
                 run_scales_lockstep(h, OPOSE_NET_BODY, fd, frame_stride, row_stride, N, H, W, gs, p);

@@ -100,19 +100,23 @@ def _host_poses(frames, body, hand, recpoint, mode, batch):
 class _DeviceIngest(object):
     """Two pinned host frame buffers -> two device frame buffers (one copy stream each) ->
     Body.infer_records(pipeline=True) -> records downloaded to pinned host memory on the
-    handle's stream; at most two batches in flight."""
+    handle's stream; at most two batches in flight.
+
+    A frame whose peaks or people overflow the record capacity (the reference has no limit) is
+    run again through Body.batch, which grows the capacity and retries like Body(); later
+    batches then get records of the grown size (a batch decodes with the layout it was
+    submitted with)."""
 
     def __init__(self, body, batch, H, W):
         import torch
         self.torch = torch
         self.body = body
-        dev = torch.device("cuda", body.handle.device)
-        rb = body.handle.record_bytes()
+        self.batch = batch
+        self.devc = torch.device("cuda", body.handle.device)
         self.host = [torch.empty((batch, H, W, 3), dtype=torch.uint8).pin_memory() for _ in range(2)]
-        self.dev = [torch.empty((batch, H, W, 3), dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.rdev = [torch.empty((batch, rb), dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.rhost = [torch.empty((batch, rb), dtype=torch.uint8).pin_memory() for _ in range(2)]
-        self.cps = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        self.dev = [torch.empty((batch, H, W, 3), dtype=torch.uint8, device=self.devc) for _ in range(2)]
+        self.rdev, self.rhost, self.layout = [None, None], [None, None], [None, None]
+        self.cps = [torch.cuda.Stream(device=self.devc) for _ in range(2)]
         self.up_done = [None, None]    # upload of buffer i finished with host[i]
         self.rec_done = [None, None]   # records of buffer i on the host
         self.lib = body.handle.torch_stream()
@@ -122,6 +126,11 @@ class _DeviceIngest(object):
         n = len(frames)
         if self.up_done[i] is not None:
             self.up_done[i].synchronize()  # host[i] free: its previous upload completed
+        rb = self.body.handle.record_bytes()
+        if self.rdev[i] is None or self.rdev[i].shape[1] != rb:  # (first use, or the capacity grew)
+            self.rdev[i] = torch.empty((self.batch, rb), dtype=torch.uint8, device=self.devc)
+            self.rhost[i] = torch.empty((self.batch, rb), dtype=torch.uint8).pin_memory()
+        self.layout[i] = (self.body.peaks_per_part, self.body.max_people)
         np.stack(frames, out=self.host[i][:n].numpy())
         cp = self.cps[i]
         cp.wait_stream(self.lib)  # the call that last read dev[i] / wrote rdev[i] is done with them
@@ -136,9 +145,21 @@ class _DeviceIngest(object):
             self.rec_done[i] = torch.cuda.Event()
             self.rec_done[i].record(self.lib)
 
-    def results(self, i, n):
+    def results(self, i, frames):
+        from . import _native
         self.rec_done[i].synchronize()
-        return [self.body._decode(r) for r in self.rhost[i][:n].numpy()]
+        out = []
+        for r, f in zip(self.rhost[i][:len(frames)].numpy(), frames):
+            status, cand, subset = _native.decode_record(r, *self.layout[i])
+            if status == _native.OPOSE_E_CAPACITY:
+                out.extend(self.body.batch(np.ascontiguousarray(f)[None]))
+            elif status == _native.OPOSE_E_ASSEMBLY:
+                raise IndexError("list assignment index out of range")  # src/body.py:170-173
+            elif status != 0:
+                raise _native.OposeError(status, "frame failed")
+            else:
+                out.append((cand, subset))
+        return out
 
 
 def _device_poses(frames, body, hand, recpoint, mode, batch):
@@ -154,12 +175,12 @@ def _device_poses(frames, body, hand, recpoint, mode, batch):
         ing.submit(i, b)
         if pending is not None:  # the previous batch's poses while this one runs on the GPU
             pi, pframes = pending
-            out.append(poses_from_results(ing.results(pi, len(pframes)), pframes, hand, mode))
+            out.append(poses_from_results(ing.results(pi, pframes), pframes, hand, mode))
         pending = (i, b)
         k += 1
     if pending is not None:
         pi, pframes = pending
-        out.append(poses_from_results(ing.results(pi, len(pframes)), pframes, hand, mode))
+        out.append(poses_from_results(ing.results(pi, pframes), pframes, hand, mode))
     return out
 
 

@@ -44,6 +44,9 @@ def timed(fn, iters, warm=2):
     return float(np.median(t)) * 1e3
 
 
+SKIP = set(filter(None, os.environ.get("BC_SKIP", "").split(",")))  # stages to leave out (diagnosis)
+
+
 def main():
     rng = np.random.default_rng(3)
     out = {}
@@ -64,6 +67,9 @@ def main():
 
     # C3
     crop = rng.integers(0, 256, (368, 368, 3), dtype=np.uint8)
+    if "c3" in SKIP:
+        out["C3_hand_latency_ms"] = timed(lambda: hand(crop), 10)
+        return c5(out, rng, dev)
     out["C3_hand_latency_ms"] = timed(lambda: hand(crop), 10)
     n_hands = []
 
@@ -116,6 +122,10 @@ def main():
     out["fast_mode_batch_body_frames_per_s"] = 32 / (ms * 1e-3)
     out["fast_mode_status_nonzero"] = int((recb.view(torch.int32)[:, 0] != 0).sum().item())
 
+    return c5(out, rng, dev)
+
+
+def c5(out, rng, dev):
     # C5
     # C5_OUT_SCALE: the heat conv's per-channel affine measured at 1080p / 4 scales (~190 peaks,
     # ~10 people per frame; src/weights.py).  The network (value independent) is >97 % of this
@@ -151,10 +161,10 @@ def main():
     out["C5_status_nonzero"] = int((st != 0).sum())
     out["C5_mean_peaks_people"] = rec5.view(torch.int32)[:, 1:3].float().mean(0).cpu().tolist()
 
-    # the same C5 work with the four scales' networks in lockstep (OPOSE_LOCKSTEP=2: one conv
-    # launch per layer for all scales, as Hand() runs; not the default for Body because the
-    # scale-sharded split would then no longer reproduce Body(frame) bit for bit)
-    os.environ["OPOSE_LOCKSTEP"] = "2"
+    # the same C5 work with one network per scale on concurrent streams (OPOSE_LOCKSTEP=0; the
+    # default runs the four scales' networks in lockstep, one conv launch per layer, DESIGN §4.3;
+    # both give the same maps bit for bit)
+    os.environ["OPOSE_LOCKSTEP"] = "0"
     try:
         body5l = Body(seeded_state_dict("body", 0, out_scale=cal), scale_search=(0.5, 1.0, 1.5, 2.0))
     finally:
@@ -164,12 +174,12 @@ def main():
         body5l.infer_records(f5, rec5)
         body5l.handle.synchronize()
     ms = timed(step5l, 5, warm=1)
-    out["C5_lockstep_frames_per_s_per_gpu"] = B / (ms * 1e-3)
+    out["C5_per_scale_streams_frames_per_s_per_gpu"] = B / (ms * 1e-3)
 
     def one5l():
         body5l.infer_records(f5[:1].contiguous(), rec5[:1])
         body5l.handle.synchronize()
-    out["C5_lockstep_single_frame_latency_ms"] = timed(one5l, 10, warm=2)
+    out["C5_per_scale_streams_single_frame_latency_ms"] = timed(one5l, 10, warm=2)
     del body5l
 
     # C5 single-frame latency: all four scales on one GPU vs the scale-sharded split

@@ -185,3 +185,25 @@ def test_rccl_exchange_moves_the_halo_rows(bodies, frame):
     dev = b.band_maps(torch.from_numpy(frame).cuda(), 3, 30, 60, "rccl")
     assert np.array_equal(dev.cpu().numpy(), ref)
     b.handle.set_band_peers(None, None)
+
+
+def test_body_lockstep_equals_per_scale_networks(frame):
+    """A multi-scale Body's four networks in lockstep (default: one conv launch per layer for all
+    scales, their work units scheduled together) against one network per scale on concurrent
+    streams (OPOSE_LOCKSTEP=0): the same (candidate, subset) bit for bit."""
+    from src.body import Body
+    from src.weights import c5_out_scale, seeded_state_dict
+    sd = seeded_state_dict("body", 0, out_scale=c5_out_scale())
+    lock = Body(sd, scale_search=SCALES)
+    old = os.environ.get("OPOSE_LOCKSTEP")
+    os.environ["OPOSE_LOCKSTEP"] = "0"
+    try:
+        per = Body(sd, scale_search=SCALES)
+    finally:
+        if old is None:
+            del os.environ["OPOSE_LOCKSTEP"]
+        else:
+            os.environ["OPOSE_LOCKSTEP"] = old
+    (ca, sa), = lock.batch(frame[None])
+    (cb, sb), = per.batch(frame[None])
+    assert len(ca) > 0 and np.array_equal(ca, cb) and np.array_equal(sa, sb)
