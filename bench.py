@@ -132,7 +132,7 @@ PEAK_HBM_GBS = 8000.0
 # exceed it on sparse maps).
 GAUSS_OPS_PER_PIXEL = 2 * 37
 PEAK_F64_OPS = 39.3e12
-LATENCY_STAGES = ("peaks_finalize", "paf_score", "limb_greedy", "assemble", "hand_cc")
+LATENCY_STAGES = ("peaks_finalize", "limb_greedy", "assemble", "hand_cc")
 
 
 def stage_roofline(prof):

@@ -57,15 +57,23 @@ struct ConvArgs {
 // slice, o0 includes the slice's first group).  Two layouts are used:
 //  * dense  [N][Cg][H*W]:  fs = Cg*H*W, gs = H*W, rs = W, o0 = goff*H*W (trunk activations);
 //  * padded (X6P, the low-resolution CPM stage buffers): per group one tall image of the N
-//    frames stacked with 3 zero rows above, between and below them and 3 zero units between
-//    consecutive rows (row pitch P = W + 3, pixel (n, y, x) at row 3 + n*(H+3) + y, column
-//    3 + x), plus one zero row at the end: every tap of a 7x7 / 3x3 / 1x1 'same' conv is a
-//    constant shift dy*P + dx of the pixel's unit, and the window of a run of consecutive
-//    pixels is contiguous across rows and frames (conv7_win_x6).  fs = (H+3)*P, gs =
-//    (N*(H+3)+4)*P, rs = P, o0 = goff*gs + 3*P + 3.  The zero units are never written.
+//    frames stacked with 3 zero rows above, between and below them and kX6PPad zero units
+//    between consecutive rows (row pitch P = W + kX6PPad, pixel (n, y, x) at row 3 + n*(H+3) + y,
+//    column 3 + x: 3 zero units before a row's pixels, kX6PPad - 3 after them), plus one zero row
+//    at the end: every tap of a 7x7 / 3x3 / 1x1 'same' conv is a constant shift dy*P + dx of the
+//    pixel's unit, and the window of a run of consecutive pixels is contiguous across rows and
+//    frames (conv_win_x6).  fs = (H+3)*P, gs = (N*(H+3)+4)*P, rs = P, o0 = goff*gs + 3*P + 3.  The
+//    zero units are never written.
 struct X6Layout {
     uint32_t fs, gs, rs, o0;
 };
+
+// Zero units per X6P row: 16, so that P - W is a multiple of 16 units.  A window kernel's B
+// fragment reads 16 consecutive pixels per ds_read_b128 lane group, and a group that crosses a row
+// end then jumps P - W units: a multiple of 16 keeps the 16 units on 16 distinct 16-byte slots of
+// the 256-byte bank row (3 zero units made 2-way conflicts).
+constexpr int kX6PPad = 16;
+__host__ __device__ inline int x6p_pitch(int W) { return W + kX6PPad; }
 
 struct X6Group {
     const uint8_t* in;     // X6 buffer (plane 0)

@@ -409,13 +409,14 @@ void x6_pack_weights_pairs(const float* w, int cout, int cin, int ks, int Mpad, 
         }
 }
 
-// window capacities (units per (piece, group)): LDS = 2 weight stages (48 KB) + 2 x 3 x WMAX units
-constexpr int kWinSmall = 768, kWinLarge = 1088;
+// window capacities (units per (piece, group)): LDS = 3 weight stages (72 KB) + 2 x 3 x 832 units
+// (78 KB; the bench's 23 x 41 frames at P = 57: <= 801 units), or 2 stages + 2 x 3 x 1088 units
+constexpr int kWinSmall = 832, kWinLarge = 1088;
 constexpr int kWinStagesSmall = 3;  // weight stages of the small-window kernels (2: 2,021 vs 2,048 frames/s)
 
 // largest window (units) a tile of PT pixels needs on an N x H x W batch for a KS x KS conv
 int conv_win_units(int N, int H, int W, int ks, int pt) {
-    const int HW = H * W, P = W + 3, npix = N * HW, pad = ks / 2;
+    const int HW = H * W, P = x6p_pitch(W), npix = N * HW, pad = ks / 2;
     int worst = 0;
     for (int p0 = 0; p0 < npix; p0 += pt) {
         const int p1 = std::min(p0 + pt, npix) - 1;
@@ -426,13 +427,13 @@ int conv_win_units(int N, int H, int W, int ks, int pt) {
 }
 
 bool conv_win_fits(int N, int H, int W, int ks) {
-    return (ks == 3 || ks == 7) && W + 3 <= 1024 && conv_win_units(N, H, W, ks, 256) <= kWinLarge;
+    return (ks == 3 || ks == 7) && x6p_pitch(W) <= 1024 && conv_win_units(N, H, W, ks, 256) <= kWinLarge;
 }
 
 bool conv_win_fits_rows(int W, int ks) {
     // a run starting at column x spans (x + 255) / W + 1 rows: at most (W + 254) / W + 1
     const int pad = ks / 2, span = (W + 254) / W;
-    return (ks == 3 || ks == 7) && W + 3 <= 1024 && (span + 2 * pad + 1) * (W + 3) + pad <= kWinLarge;
+    return (ks == 3 || ks == 7) && x6p_pitch(W) <= 1024 && (span + 2 * pad + 1) * x6p_pitch(W) + pad <= kWinLarge;
 }
 
 void launch_conv_win_x6(const X6Args& a0, hipStream_t st) {
@@ -442,7 +443,7 @@ void launch_conv_win_x6(const X6Args& a0, hipStream_t st) {
     int need = 0;
     for (int g = 0; g < a.ngroups; ++g) {
         const X6Group& G = a.g[g];
-        if (G.in_l.rs != (uint32_t)G.W + 3 || G.in_l.fs != (uint32_t)(G.H + 3) * G.in_l.rs)
+        if (G.in_l.rs != (uint32_t)x6p_pitch(G.W) || G.in_l.fs != (uint32_t)(G.H + 3) * G.in_l.rs)
             throw std::invalid_argument("conv_win_x6: input is not X6P");
         need = std::max(need, conv_win_units(G.N, G.H, G.W, a.ks, 256));
     }

@@ -552,9 +552,9 @@ struct PadBufs {
     int planes[8];
 };
 
-__global__ __launch_bounds__(256) void x6p_clear_pads_kernel(PadBufs b, size_t plane, int N, int H, int P) {
+__global__ __launch_bounds__(256) void x6p_clear_pads_kernel(PadBufs b, size_t plane, int N, int H, int W, int P) {
     const int pad_rows = 3 * N + 4;
-    const size_t per_plane = (size_t)pad_rows * P + (size_t)N * H * 3;
+    const size_t per_plane = (size_t)pad_rows * P + (size_t)N * H * (P - W);
     uint4* buf = b.p[blockIdx.y];
     const size_t total = per_plane * b.planes[blockIdx.y];
     const uint4 z = make_uint4(0u, 0u, 0u, 0u);
@@ -566,11 +566,12 @@ __global__ __launch_bounds__(256) void x6p_clear_pads_kernel(PadBufs b, size_t p
             const int pr = (int)(u / P), c = (int)(u - (size_t)pr * P);
             const int row = pr < 3 ? pr : 3 + ((pr - 3) / 3) * (H + 3) + H + (pr - 3) % 3;
             unit = (size_t)(pr >= 3 * N + 3 ? 3 + N * (H + 3) + (pr - 3 * N - 3) : row) * P + c;
-        } else {  // the 3 units at the start of a pixel row
+        } else {  // the P - W zero units of a pixel row: 3 before its pixels, the rest after them
             u -= (size_t)pad_rows * P;
-            const int pr = (int)(u / 3), c = (int)(u - (size_t)pr * 3);
+            const int pw = P - W;
+            const int pr = (int)(u / pw), c = (int)(u - (size_t)pr * pw);
             const int n = pr / H, y = pr - n * H;
-            unit = (size_t)(3 + n * (H + 3) + y) * P + c;
+            unit = (size_t)(3 + n * (H + 3) + y) * P + (c < 3 ? c : c + W);
         }
         buf[pl * plane + unit] = z;
     }
@@ -578,7 +579,7 @@ __global__ __launch_bounds__(256) void x6p_clear_pads_kernel(PadBufs b, size_t p
 
 void launch_x6p_clear_pads(uint8_t* const* bufs, const int* planes, int nbufs, int N, int H, int W, hipStream_t st) {
     if (nbufs < 1 || nbufs > 8) throw std::invalid_argument("x6p_clear_pads: 1..8 buffers");
-    const int P = W + 3;
+    const int P = x6p_pitch(W);
     const size_t plane = (size_t)(N * (H + 3) + 4) * P;
     PadBufs b{};
     int most = 0;
@@ -587,9 +588,9 @@ void launch_x6p_clear_pads(uint8_t* const* bufs, const int* planes, int nbufs, i
         b.planes[i] = planes[i];
         most = std::max(most, planes[i]);
     }
-    const size_t pads = ((size_t)(3 * N + 4) * P + (size_t)N * H * 3) * most;
+    const size_t pads = ((size_t)(3 * N + 4) * P + (size_t)N * H * (P - W)) * most;
     hipLaunchKernelGGL(x6p_clear_pads_kernel, dim3(std::min(grid_for(pads), 2048), nbufs), dim3(256), 0, st, b, plane,
-                       N, H, P);
+                       N, H, W, P);
 }
 
 // Halo rows of a row band (engine.cpp band_halo): 3 consecutive rows of groups [g0, g0 + ng) of

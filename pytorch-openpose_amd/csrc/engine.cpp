@@ -24,6 +24,7 @@
 #include <functional>
 #include <initializer_list>
 #include <map>
+#include <mutex>
 #include <memory>
 #include <string>
 #include <queue>
@@ -99,6 +100,41 @@ std::vector<Spec> state_dict_order(int net) {
 }
 
 int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+// ---------------------------------------------------------------- streams
+// Streams come from a process-wide pool and go back to it when a handle is destroyed, instead of
+// hipStreamDestroy: on this stack a graph captured after another handle destroyed its streams
+// crashed in hipGraphLaunch (round 4, scripts/r4_c5three.py).  A pooled stream is drained before
+// it is reused.
+struct StreamPool {
+    std::mutex mu;
+    std::map<std::pair<int, int>, std::vector<hipStream_t>> free;  // (device, priority) -> streams
+};
+StreamPool& stream_pool() {
+    static StreamPool* p = new StreamPool();  // never destroyed: handles may outlive static teardown
+    return *p;
+}
+hipError_t pooled_stream(hipStream_t* s, int priority) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    {
+        std::lock_guard<std::mutex> g(stream_pool().mu);
+        auto& v = stream_pool().free[{dev, priority}];
+        if (!v.empty()) {
+            *s = v.back();
+            v.pop_back();
+            return hipSuccess;
+        }
+    }
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, priority);
+}
+void return_stream(hipStream_t s, int device, int priority) {
+    if (!s) return;
+    (void)hipStreamSynchronize(s);
+    std::lock_guard<std::mutex> g(stream_pool().mu);
+    stream_pool().free[{device, priority}].push_back(s);
+}
 
 // ---------------------------------------------------------------- device memory helpers
 // Bumped whenever device memory that a captured hipGraph may reference is (re)allocated:
@@ -314,6 +350,7 @@ struct opose_ctx {
     // point used the shared network workspace there since (main_dirty).  Every call ends with
     // `stream` ordered after its own network part.
     hipStream_t nstream = nullptr;
+    int nstream_prio = 0;
     hipEvent_t ev_net = nullptr, ev_main = nullptr, ev_post[2] = {nullptr, nullptr};
     // opose_wait_stream / opose_signal_stream / opose_set_stream: ordering against streams the
     // caller owns (a framework's current stream)
@@ -392,16 +429,16 @@ struct opose_ctx {
         for (auto& kv : graphs)
             if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
         graphs.clear();
-        if (nstream) (void)hipStreamDestroy(nstream);
+        return_stream(nstream, device, nstream_prio);
         for (hipEvent_t e : {ev_net, ev_main, ev_post[0], ev_post[1], ev_ext, ev_sig, ev_fork})
             if (e) (void)hipEventDestroy(e);
         for (int i = 0; i < kMaxScales; ++i) {
-            if (sstream[i]) (void)hipStreamDestroy(sstream[i]);
+            return_stream(sstream[i], device, 0);
             if (ev_join[i]) (void)hipEventDestroy(ev_join[i]);
         }
         for (int* p : sched_mem) (void)hipFree(p);
         for (auto e : event_pool) (void)hipEventDestroy(e);
-        if (own_stream) (void)hipStreamDestroy(own_stream);
+        return_stream(own_stream, device, 0);
     }
 };
 
@@ -810,10 +847,10 @@ static XAct x6act(uint8_t* p, int cg, int goff, int N, int H, int W) {
 }
 
 // padded X6P (common.h): units per (piece, group) plane
-static size_t x6p_plane(int N, int H, int W) { return (size_t)(N * (H + 3) + 4) * (W + 3); }
+static size_t x6p_plane(int N, int H, int W) { return (size_t)(N * (H + 3) + 4) * x6p_pitch(W); }
 
 static XAct x6pact(uint8_t* p, int cg, int goff, int N, int H, int W) {
-    const size_t P = (size_t)W + 3, plane = x6p_plane(N, H, W);
+    const size_t P = (size_t)x6p_pitch(W), plane = x6p_plane(N, H, W);
     XAct a;
     a.p = p;
     a.ps = checked_ps((size_t)cg * plane * 16);
@@ -952,6 +989,11 @@ static int slab_count(opose_ctx* h, const DevConv* c, bool win, int N, int H, in
     if (c->net == OPOSE_NET_HAND) {
         if (c->ks != 7 || !win) return 1;
         const double T = std::ceil(npix / 256.0) * mr;
+        if (const char* e = getenv("OPOSE_HAND_SLABS")) {  // TEMP sweep
+            int v[7] = {16, 12, 8, 7, 4, 2, 1};
+            sscanf(e, "%d,%d,%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5], &v[6]);
+            return clampS(T < 6 ? v[0] : T < 12 ? v[1] : T < 30 ? v[2] : T < 60 ? v[3] : T < 120 ? v[4] : T < 240 ? v[5] : v[6]);
+        }
         return clampS(T < 6 ? 16 : T < 12 ? 12 : T < 30 ? 8 : T < 60 ? 7 : T < 120 ? 4 : T < 240 ? 2 : 1);
     }
     const int mult = c->pair ? 2 : 1;
@@ -1013,7 +1055,6 @@ static opose_ctx::ConvPlan plan_launch(opose_ctx* h, const std::vector<ConvSeg>&
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         OPOSE_HIP_CHECK(hipStreamIsCapturing(h->stream, &cs));
         if (cs != hipStreamCaptureStatusNone) return best;  // (captured: contiguous unit ranges, same sums)
-        if (getenv("OPOSE_NO_SCHED")) { h->plans[key] = best; return best; }  // TEMP diag
         std::vector<int> flat(best.grid + 1, 0);
         for (int w = 0; w < best.grid; ++w) flat[w + 1] = flat[w] + (int)lists[w].size();
         for (const auto& L : lists) flat.insert(flat.end(), L.begin(), L.end());
@@ -1442,8 +1483,8 @@ struct Band {
 constexpr int kBandTrunkMargin = 10;
 
 // bytes of one direction of a band's halo exchange at wl columns: 3 pieces x 32 groups (the
-// widest stage tensor, 256 channels) x 3 rows x (wl + 3) units x 16 B
-static size_t band_halo_bytes(int wl) { return (size_t)3 * 32 * 3 * (wl + 3) * 16; }
+// widest stage tensor, 256 channels) x 3 rows x P units x 16 B
+static size_t band_halo_bytes(int wl) { return (size_t)3 * 32 * 3 * x6p_pitch(wl) * 16; }
 
 // bodypose_model.forward on X6 activations, every segment in lockstep; per segment the fp32
 // output in its slot's S0 with the fp32 path's layout (channel stride 185: paf [0,38), heat [38,57)).
@@ -1499,7 +1540,7 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
     // (cg groups) up / down, receive the neighbours' rows into the rows above / below the band
     auto band_halo = [&](uint8_t* buf, int cg, int g0, int ng) {
         if (!band) return;
-        const int hl = bs[0].hl, P = bs[0].wl + 3;
+        const int hl = bs[0].hl, P = x6p_pitch(bs[0].wl);
         const size_t plane = x6p_plane(1, hl, bs[0].wl), bytes = (size_t)9 * ng * P * 16;
         const int mask = (band->r0 > 0 ? 1 : 0) | (band->r1 < hl ? 2 : 0);
         if (!mask) return;
@@ -1798,7 +1839,12 @@ static ScaleGeom geom(double s, const opose_params& p, int H, int W) {
     return g;
 }
 
-// post-network body path from per-scale x8 maps (mids) to records
+// Body mid set of one scale: the x8 heat channels [N][18][Hs][Ws] (read whole by the heat resize),
+// then the network's low-res PAF channels [N][38][hl][wl], whose x8 values paf_score evaluates at
+// its sample points only (the x8 PAF maps are never written: PafScales::low)
+static size_t body_mid_heat(int N, const ScaleGeom& g) { return (size_t)N * 18 * g.Hs * g.Ws; }
+
+// post-network body path from per-scale mid sets (body_to_mid) to records
 static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vector<ScaleGeom>& gs,
                              const opose_params& p, uint8_t* rec_dev) {
     const RecordLayout L = make_record_layout(h->ppp, h->maxp);
@@ -1807,13 +1853,17 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     PafScales S{};
     for (int s = 0; s < ns; ++s) {
         S.mid[s] = h->mid(s).ensure<float>(0, h->stream);
+        S.low[s] = S.mid[s] + body_mid_heat(N, gs[s]);
         S.hs[s] = gs[s].Hs;
         S.ws[s] = gs[s].Ws;
+        S.hl[s] = gs[s].hl;
+        S.wl[s] = gs[s].wl;
         S.sy[s] = gs[s].up_sy;
         S.sx[s] = gs[s].up_sx;
     }
     S.n = ns;
-    S.cm = 56;
+    S.cm = 18;
+    S.lcm = 38;
     S.H = H;
     S.W = W;
     int* cnt = h->cnt.ensure<int>((size_t)N * 18, h->stream);
@@ -1836,7 +1886,7 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
         // full-resolution part-map pixel (bench.py GAUSS_OPS_PER_PIXEL); bytes: the x8 heat
         // channels the tiles read
         h->prof_begin(pe, "gauss_nms_resize", 74.0 * N * 18 * (double)H * W, (double)N * 18 * 4.0 * gs[0].Hs * gs[0].Ws);
-        launch_gauss_nms_resize(S.mid[0], 56, 38, 18, N, gs[0].Hs, gs[0].Ws, H, W, gs[0].up_sy, gs[0].up_sx, p.thre1,
+        launch_gauss_nms_resize(S.mid[0], 18, 0, 18, N, gs[0].Hs, gs[0].Ws, H, W, gs[0].up_sy, gs[0].up_sx, p.thre1,
                                 cap, cnt, list, lscore, h->stream);
         h->prof_end(pe);
     } else {
@@ -1845,10 +1895,10 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
         h->prof_begin(pe, "heat_full", 0,
                       (double)N * 18 * (H * W * (f32 ? 4.0 : 8.0) * (s ? 2 : 1) + 4.0 * gs[s].Hs * gs[s].Ws));
         if (f32)
-            launch_heat_full_f32(S.mid[s], 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx,
+            launch_heat_full_f32(S.mid[s], 18, 0, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx,
                                  reinterpret_cast<float*>(avg), h->stream);
         else
-            launch_heat_full(S.mid[s], 56, 38, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx, ns, s > 0,
+            launch_heat_full(S.mid[s], 18, 0, 18, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx, ns, s > 0,
                              avg, h->stream);
         h->prof_end(pe);
     }
@@ -1859,7 +1909,10 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     h->prof_begin(pe, "peaks_finalize", 0, 0);
     launch_peaks_finalize(cnt, list, lscore, N, H, W, L, rec_dev, pos, pcnt, h->stream);
     h->prof_end(pe);
-    h->prof_begin(pe, "paf_score", 0, 0);
+    // bytes: the low-res PAF channels, read once from HBM (every sample after the first hits L2)
+    double paf_bytes = 0;
+    for (int s = 0; s < ns; ++s) paf_bytes += (double)N * 38 * 4 * gs[s].hl * gs[s].wl;
+    h->prof_begin(pe, "paf_score", 0, paf_bytes);
     launch_paf_score(S, pos, pcnt, N, cap, p.thre2, score, h->stream);
     h->prof_end(pe);
     h->prof_begin(pe, "limb_greedy", 0, 0);
@@ -1875,6 +1928,18 @@ static void upsample_to_mid(opose_ctx* h, int s, const float* maps, int cstride,
     ProfEntry pe;
     h->prof_begin(pe, "upsample8", 0, (double)N * C * g.Hs * g.Ws * 4);
     launch_upsample8(maps, cstride, 0, C, N, g.hl, g.wl, g.Hs, g.Ws, mid, h->stream);
+    h->prof_end(pe);
+}
+
+// body maps (PAF channels 0..37, heat 38..55 of [N][cstride][hl][wl]) -> mid set s (body_mid_heat)
+static void body_to_mid(opose_ctx* h, int s, const float* maps, int cstride, int N, const ScaleGeom& g) {
+    const size_t heat = body_mid_heat(N, g), lp = (size_t)g.hl * g.wl;
+    float* mid = h->mid(s).ensure<float>(heat + (size_t)N * 38 * lp, h->stream);
+    ProfEntry pe;
+    h->prof_begin(pe, "upsample8", 0, (double)heat * 4 + (double)N * 56 * lp * 4 + (double)N * 38 * lp * 4);
+    launch_upsample8(maps, cstride, 38, 18, N, g.hl, g.wl, g.Hs, g.Ws, mid, h->stream);
+    OPOSE_HIP_CHECK(hipMemcpy2DAsync(mid + heat, 38 * lp * 4, maps, (size_t)cstride * lp * 4, 38 * lp * 4, N,
+                                     hipMemcpyDeviceToDevice, h->stream));
     h->prof_end(pe);
 }
 
@@ -1897,7 +1962,10 @@ static void run_scales_lockstep(opose_ctx* h, int net, const uint8_t* fd, int64_
     }
     const std::vector<float*> outs = net == OPOSE_NET_BODY ? body_net_x6(h, segs) : hand_net_x6(h, segs);
     for (size_t s = 0; s < gs.size(); ++s)
-        upsample_to_mid(h, (int)s, outs[s], net == OPOSE_NET_BODY ? 185 : 150, N, gs[s], net == OPOSE_NET_BODY ? 56 : 21);
+        if (net == OPOSE_NET_BODY)
+            body_to_mid(h, (int)s, outs[s], 185, N, gs[s]);
+        else
+            upsample_to_mid(h, (int)s, outs[s], 150, N, gs[s], 21);
 }
 
 // bytes a strided uint8 [N][H][W][3] host view spans: the last row ends 3*W bytes after its start,
@@ -2087,7 +2155,7 @@ int opose_create(int device, opose_t** out) {
     *out = nullptr;
     auto* h = new opose_ctx();
     h->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || pooled_stream(&h->own_stream, 0) != hipSuccess) {
         delete h;
         return OPOSE_E_HIP;
     }
@@ -2354,7 +2422,7 @@ static void run_scales_concurrently(opose_ctx* h, int ns, const std::function<vo
     OPOSE_HIP_CHECK(hipEventRecord(h->ev_fork, main));
     for (int s = 1; s < ns; ++s) {
         if (!h->sstream[s]) {
-            OPOSE_HIP_CHECK(hipStreamCreateWithFlags(&h->sstream[s], hipStreamNonBlocking));
+            OPOSE_HIP_CHECK(pooled_stream(&h->sstream[s], 0));
             OPOSE_HIP_CHECK(hipEventCreateWithFlags(&h->ev_join[s], hipEventDisableTiming));
         }
         OPOSE_HIP_CHECK(hipStreamWaitEvent(h->sstream[s], h->ev_fork, 0));
@@ -2385,7 +2453,8 @@ static void pipelined_body(opose_ctx* h, int N, int H, int W, const std::vector<
         // the network stream gets the higher priority: its conv grids should not wait for
         // post-network workgroups that can run on whatever CUs are left (network high / post
         // high / both default measured the same)
-        OPOSE_HIP_CHECK(hipStreamCreateWithPriority(&h->nstream, hipStreamNonBlocking, hi));
+        OPOSE_HIP_CHECK(pooled_stream(&h->nstream, hi));
+        h->nstream_prio = hi;
         for (hipEvent_t* e : {&h->ev_net, &h->ev_main, &h->ev_post[0], &h->ev_post[1]})
             OPOSE_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
@@ -2445,7 +2514,7 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
                               g.Wp, (float)p.pad_value / 256.f - 0.5f, x, h->stream);
             h->prof_end(pe);
             float* S = body_net(h, x, N, g.Hp, g.Wp);
-            upsample_to_mid(h, s, S, 185, N, g, 56);
+            body_to_mid(h, s, S, 185, N, g);
         };
         const bool lockstep = h->x6 && h->lockstep && p.n_scales > 1;
         auto net_part = [&] {
@@ -2502,7 +2571,7 @@ int opose_body_post(opose_t* h, const float* maps, int N, int hl, int wl, int pa
         g.Ws = g.Wp - pad_right;
         g.up_sy = 1.0 / ((double)H / g.Hs);
         g.up_sx = 1.0 / ((double)W / g.Ws);
-        upsample_to_mid(h, 0, md, 57, N, g, 56);
+        body_to_mid(h, 0, md, 57, N, g);
         uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)
                                                   : h->records.ensure<uint8_t>(L.bytes * N, h->stream);
         body_post_common(h, N, H, W, {g}, p, rec);
@@ -2678,7 +2747,7 @@ int opose_body_post_scales(opose_t* h, const float* const* maps, const int* hl, 
                 OPOSE_HIP_CHECK(hipMemcpyAsync(buf, maps[s], n_in * 4, hipMemcpyHostToDevice, h->stream));
                 md = buf;
             }
-            upsample_to_mid(h, s, md, 57, N, g, 56);
+            body_to_mid(h, s, md, 57, N, g);
             gs.push_back(g);
         }
         uint8_t* rec = (flags & OPOSE_OUT_DEVICE) ? static_cast<uint8_t*>(records)

@@ -8,12 +8,18 @@ namespace opose {
 
 constexpr int kMaxScales = 8;
 
-// x8 maps of every scale for on-demand PAF evaluation (paf_score) and hand heat
+// PAF maps of every scale for on-demand evaluation at paf_score's sample points: either the x8
+// map mid[s] ([N][cm][hs][ws], channel 0 = PAF x) or, when low[s] is set, the network's low-res
+// PAF channels ([N][lcm][hl][wl]), whose x8 values are evaluated where the final resize reads them
+// (cv2.resize(fx=fy=8) then the resize to H x W, src/body.py:55-63: the same float32 expressions in
+// the same order as the staged upsample, so the same values)
 struct PafScales {
     const float* mid[kMaxScales];  // [N][cm][hs][ws] per scale
+    const float* low[kMaxScales];  // [N][lcm][hl][wl] per scale, or nullptr
     int hs[kMaxScales], ws[kMaxScales];
+    int hl[kMaxScales], wl[kMaxScales];
     double sy[kMaxScales], sx[kMaxScales];  // source step of the final resize to H x W
-    int n, cm, H, W;
+    int n, cm, lcm, H, W;
     int torch;  // 1: torch bicubic taps (Batch_body fast mode), 0: OpenCV INTER_CUBIC
 };
 

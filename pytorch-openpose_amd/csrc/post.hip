@@ -650,6 +650,82 @@ __global__ __launch_bounds__(128) void peaks_finalize(const int* __restrict__ cn
     if (threadIdx.x == 0) part_cnt[n * 18 + p] = c;
 }
 
+// value of the x8 map (cv2.resize(fx=fy=8, INTER_CUBIC) of an hl x wl plane, cropped) at (y8, x8):
+// cubic_resize_rows<0>'s horizontal-then-vertical sums, so bit-identical to the staged map
+__device__ __forceinline__ float x8_at(const float* __restrict__ low, int hl, int wl, int y8, int x8) {
+    return cubic_sample_f32(low, wl, cubic_tap(y8, 0.125, hl), cubic_tap(x8, 0.125, wl));
+}
+
+__device__ __forceinline__ float pick5(const float (&p)[5], int d) {
+    float v = p[0];
+    v = d == 1 ? p[1] : v;
+    v = d == 2 ? p[2] : v;
+    v = d == 3 ? p[3] : v;
+    v = d == 4 ? p[4] : v;
+    return v;
+}
+
+// the final resize (taps ty / tx over the x8 map) at one point of the PAF pair (chx, chx + 1), the
+// x8 values evaluated from the low-res planes lx / ly.  The 4 x 4 x8 samples read a 5 x 5 low-res
+// patch (the taps of a cubic resize are 4 consecutive indices; 4 consecutive x8 rows or columns
+// span 3/8 of a low-res step, so their 4-tap supports fall in 5 consecutive low-res rows /
+// columns), so the patch is loaded once and every horizontal sum computed once per (patch row, x8
+// column).  Each value is cubic_resize_rows<0>'s sum, then cubic_sample_f32's over those, in the
+// same order: bit-identical to resampling the staged x8 map.
+__device__ __forceinline__ void resize_x8_pair(const float* __restrict__ lx, const float* __restrict__ ly, int hl,
+                                               int wl, const CubicTap& ty, const CubicTap& tx, float& ox, float& oy) {
+    CubicTap cx[4], ry[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        cx[j] = cubic_tap(tx.i[j], 0.125, wl);
+        ry[j] = cubic_tap(ty.i[j], 0.125, hl);
+    }
+    const int r0 = ry[0].i[0], c0 = cx[0].i[0];
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+        const float* plane = ch ? ly : lx;
+        float hsum[4][5];  // [x8 column j][patch row k]
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const float* row = plane + (size_t)min(r0 + k, hl - 1) * wl;
+            float p[5];
+#pragma unroll
+            for (int d = 0; d < 5; ++d) p[d] = row[min(c0 + d, wl - 1)];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float v = pick5(p, cx[j].i[0] - c0) * cx[j].c[0];
+                v = v + pick5(p, cx[j].i[1] - c0) * cx[j].c[1];
+                v = v + pick5(p, cx[j].i[2] - c0) * cx[j].c[2];
+                v = v + pick5(p, cx[j].i[3] - c0) * cx[j].c[3];
+                hsum[j][k] = v;
+            }
+        }
+        float h[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float x8[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float o = pick5(hsum[j], ry[r].i[0] - r0) * ry[r].c[0];
+                o = o + pick5(hsum[j], ry[r].i[1] - r0) * ry[r].c[1];
+                o = o + pick5(hsum[j], ry[r].i[2] - r0) * ry[r].c[2];
+                o = o + pick5(hsum[j], ry[r].i[3] - r0) * ry[r].c[3];
+                x8[j] = o;
+            }
+            float v = x8[0] * tx.c[0];
+            v = v + x8[1] * tx.c[1];
+            v = v + x8[2] * tx.c[2];
+            v = v + x8[3] * tx.c[3];
+            h[r] = v;
+        }
+        float o = h[0] * ty.c[0];
+        o = o + h[1] * ty.c[1];
+        o = o + h[2] * ty.c[2];
+        o = o + h[3] * ty.c[3];
+        (ch ? oy : ox) = o;
+    }
+}
+
 // grid (frames * 19 limbs, blocks per limb); pair (i, j) -> score[n][k][i*nB + j]
 // (-inf when criterion1/criterion2 fail; src/body.py:137-141).  A thread per (pair, sample): the
 // ten samples of a pair are evaluated by ten lanes (each a cubic resample chain of dependent
@@ -695,7 +771,18 @@ __global__ __launch_bounds__(256) void paf_score(PafScales S, const int* __restr
                 const size_t plane = (size_t)S.hs[s] * S.ws[s];
                 const float* mx = S.mid[s] + ((size_t)n * S.cm + chx) * plane;
                 float vx_, vy_;
-                if (S.hs[s] == S.H && S.ws[s] == S.W) {
+                if (S.low[s]) {  // x8 values from the low-res PAF channels (L2-resident)
+                    const size_t lp = (size_t)S.hl[s] * S.wl[s];
+                    const float* lx = S.low[s] + ((size_t)n * S.lcm + chx) * lp;
+                    if (S.hs[s] == S.H && S.ws[s] == S.W) {
+                        vx_ = x8_at(lx, S.hl[s], S.wl[s], Y, X);
+                        vy_ = x8_at(lx + lp, S.hl[s], S.wl[s], Y, X);
+                    } else {
+                        const CubicTap ty = cubic_tap(Y, S.sy[s], S.hs[s]);
+                        const CubicTap tx = cubic_tap(X, S.sx[s], S.ws[s]);
+                        resize_x8_pair(lx, lx + lp, S.hl[s], S.wl[s], ty, tx, vx_, vy_);
+                    }
+                } else if (S.hs[s] == S.H && S.ws[s] == S.W) {
                     vx_ = mx[(size_t)Y * S.ws[s] + X];
                     vy_ = mx[plane + (size_t)Y * S.ws[s] + X];
                 } else {

@@ -118,6 +118,39 @@ def test_hand_scale_streams_bit_identical():
     assert a.dtype == b.dtype and np.array_equal(a, b)
 
 
+def test_graph_replay_equals_eager():
+    """Body() / Hand() calls replay a captured hipGraph from the third call with the same shapes
+    on; a handle created with OPOSE_NO_GRAPH=1 runs every call eagerly.  Replays (a two-scale
+    lockstep pyramid with its slab schedules, and a hand pyramid) equal the eager calls exactly."""
+    from src.body import Body
+    from src.hand import Hand
+    from src.weights import seeded_state_dict
+    rng = np.random.default_rng(15)
+    img = rng.integers(0, 256, (184, 232, 3), dtype=np.uint8)
+    crop = rng.integers(0, 256, (128, 128, 3), dtype=np.uint8)
+    bsd, hsd = seeded_state_dict("body", 0), seeded_state_dict("hand", 0)
+
+    def make(env):
+        old = os.environ.get("OPOSE_NO_GRAPH")
+        if env:
+            os.environ["OPOSE_NO_GRAPH"] = "1"
+        try:
+            return Body(bsd, scale_search=(0.5, 1.0)), Hand(hsd)
+        finally:
+            if old is None:
+                os.environ.pop("OPOSE_NO_GRAPH", None)
+            else:
+                os.environ["OPOSE_NO_GRAPH"] = old
+    gb, gh = make(False)
+    eb, eh = make(True)
+    ref_b, ref_h = eb(img), eh(crop)
+    for _ in range(4):
+        cand, sub = gb(img)
+        assert np.array_equal(cand, ref_b[0]) and np.array_equal(sub, ref_b[1])
+        pk = gh(crop)
+        assert pk.dtype == ref_h.dtype and np.array_equal(pk, ref_h)
+
+
 def test_forward_waits_for_half_input(body):
     x = torch.from_numpy(np.random.default_rng(6).standard_normal((1, 3, 64, 96)).astype(np.float32))
     xh = x.half()
