@@ -102,10 +102,8 @@ std::vector<Spec> state_dict_order(int net) {
 int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
 // ---------------------------------------------------------------- streams
-// Streams come from a process-wide pool and go back to it when a handle is destroyed, instead of
-// hipStreamDestroy: on this stack a graph captured after another handle destroyed its streams
-// crashed in hipGraphLaunch (round 4, scripts/r4_c5three.py).  A pooled stream is drained before
-// it is reused.
+// Streams come from a process-wide pool and go back to it when a handle is destroyed (drained
+// first), so test suites and services that create and destroy handles do not churn HIP streams.
 struct StreamPool {
     std::mutex mu;
     std::map<std::pair<int, int>, std::vector<hipStream_t>> free;  // (device, priority) -> streams
@@ -247,6 +245,9 @@ struct opose_ctx {
     // replay it (one launch instead of ~150: single-frame latency is launch bound)
     std::map<std::string, GraphEntry> graphs;
     bool use_graphs = getenv("OPOSE_NO_GRAPH") == nullptr;
+    // set while run_graphed captures: run_scales_concurrently then keeps the capture on one
+    // stream (no forked branches in any captured graph, see run_graphed)
+    bool capturing = false;
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
@@ -317,7 +318,7 @@ struct opose_ctx {
         hlab, hsums, hpeaks, hfound, list_score, hsel;
     PinnedBuf hand_out;  // Hand() peaks + found, staged for the host
     // network workspace, one set per concurrently running scale (slot s runs on scale_stream(s);
-    // slot 0 is the handle's stream): input, activations, stream-K slabs
+    // slot 0 is the handle's stream): input, activations, k-slab partials
     struct NetWS {
         DevBuf x, xband, x6in, x6A, x6B, x6P0, x6P1, x6Q0, x6Q1, x6S0, x6S1, x6T0, x6T1, x6U, bufA, bufB, S0, S1, T0, T1, U, partial;
     };
@@ -450,6 +451,8 @@ struct Act {  // a channel slice of an NCHW activation buffer
 };
 
 // --------------------------------------------------------------- conv launch planning
+// choose_tile: the fp32 MFMA path (OPOSE_CONV=f32, conv.hip stream-K) and the whole-tile choice of
+// the split-bf16 debug entry points; the split-bf16 network plans with slab_count / pick_tile
 struct TileChoice {
     int mt, pt, grid;  // tile shape, workgroups (grid == tiles: data parallel; else stream-K)
 };
@@ -905,7 +908,7 @@ static int seg_kernel(const opose_ctx* h, const ConvSeg& sg, bool pool) {
     const DevConv* c = sg.c;
     if (!h->win7 || pool || !c->wx6p || !sg.in.padded || (c->ks != 3 && c->ks != 7)) return kKernelX6;
     const long lpix = (long)sg.N * (sg.Hl ? sg.Hl : sg.H) * sg.W;
-    if (c->net == OPOSE_NET_BODY && lpix < 4096) return kKernelX6;
+    if (c->net == OPOSE_NET_BODY && lpix < 4096 && !getenv("OPOSE_SMALL_WIN")) return kKernelX6;  // TEMP env
     if (c->net == OPOSE_NET_HAND && c->ks == 3 && c->lvl == 3) return kKernelX6;
     if (sg.N == 1) return conv_win_fits_rows(sg.W, c->ks) ? kKernelWin : kKernelX6;
     if (conv_win_fits(sg.N, sg.H, sg.W, c->ks)) return kKernelWin;
@@ -917,6 +920,9 @@ static int seg_kernel(const opose_ctx* h, const ConvSeg& sg, bool pool) {
 // a 64 x 64 tile's (measured, scripts/conv_timing.py; rounds 1-2)
 static const int kX6Cfg[6][3] = {{128, 128, 1}, {128, 256, 1}, {256, 128, 1}, {128, 64, 2}, {64, 128, 2}, {64, 64, 3}};
 static const double kX6Ovh[6] = {1.5, 1.0, 0.96, 1.1, 1.1, 1.2};
+// launches of at most 16,384 columns (one small frame, C2's layers): 128x128 priced like the
+// 8-wave tiles and 64x64 higher (round 3, choose_tile: C2 1.91 -> 1.72 ms)
+static const double kX6OvhSmall[6] = {1.0, 1.0, 0.96, 1.1, 1.1, 1.6};
 
 // GEMM columns and slab count of one group of a launch
 struct ColGroup {
@@ -940,7 +946,12 @@ struct TilePick {
 };
 static TilePick pick_tile(const std::vector<ColGroup>& cg, bool win, int nK, int Mpad) {
     bool multi = false;
-    for (const ColGroup& c : cg) multi = multi || c.S > 1;
+    long cols_all = 0;
+    for (const ColGroup& c : cg) {
+        multi = multi || c.S > 1;
+        cols_all += c.cols;
+    }
+    const double* ovh = cols_all <= 16384 && !getenv("OPOSE_BIG_TBL") ? kX6OvhSmall : kX6Ovh;  // TEMP env
     TilePick best;
     for (int ci = 0; ci < 6; ++ci) {
         const int mt = win ? 128 : kX6Cfg[ci][0], pt = win ? 256 : kX6Cfg[ci][1], occ = win ? 1 : kX6Cfg[ci][2];
@@ -955,7 +966,7 @@ static TilePick pick_tile(const std::vector<ColGroup>& cg, bool win, int nK, int
         // one-slab launches: one workgroup per tile, the hardware dispatcher balancing them
         const long G = multi ? std::min<long>(units, 256L * occ) : tiles;
         const double mk = multi ? lpt_units(gs, nK, (int)G, nullptr) : (double)((tiles + 256L * occ - 1) / (256L * occ)) * nK;
-        const double unit = (mt / 64.0) * (pt / 64.0) * (win ? 0.8 : kX6Ovh[ci]) * 0.4;
+        const double unit = (mt / 64.0) * (pt / 64.0) * (win ? 0.8 : ovh[ci]) * 0.4;
         // co-resident workgroups share a CU; a lone one of a 2-3 per CU tile runs at ~60 %
         const double share = G <= 256 ? (occ >= 2 ? 1.6 : 1.0) : (multi ? std::min<double>(occ, (double)G / 256.0) : occ);
         double cost = mk * unit * share;
@@ -987,7 +998,8 @@ static int slab_count(opose_ctx* h, const DevConv* c, bool win, int N, int H, in
     const double mr = c->Mpad / 128.0;
     auto clampS = [&](long s) { return (int)std::max<long>(1, std::min<long>(s, smax)); };
     if (c->net == OPOSE_NET_HAND) {
-        if (c->ks != 7 || !win) return 1;
+        // the 7x7 stages, and conv5_3_CPM (3x3, 128 outputs: 62 whole tiles for a 368 crop)
+        if (!(c->ks == 7 && win) && !(c->ks == 3 && c->Mpad <= 128)) return 1;
         const double T = std::ceil(npix / 256.0) * mr;
         if (const char* e = getenv("OPOSE_HAND_SLABS")) {  // TEMP sweep
             int v[7] = {16, 12, 8, 7, 4, 2, 1};
@@ -2064,7 +2076,12 @@ static void batch_post_common(opose_ctx* h, int N, int H, int W, const float* ma
 }
 
 // Run `work` (device work only: kernels, device memsets/copies on h->stream, no host sync,
-// no allocation once warm) through the launch-sequence cache keyed by `key`.
+// no allocation once warm) through the launch-sequence cache keyed by `key`.  Captures stay on
+// the one stream (h->capturing: run_scales_concurrently runs its scales one after another): on
+// this stack, destroying executable graphs whose capture forked onto other streams made later
+// graph launches of other handles segfault inside hipGraphLaunch -- 2 of 2 runs of the GPU test
+// list, 0 of 2 with the forks kept out of captures or with no executable graph destroyed
+// (round 4; the eager first call of a signature still runs the scales concurrently).
 template <class F>
 static void run_graphed(opose_ctx* h, const std::string& key, F&& work) {
     if (!h->use_graphs || h->prof || !h->stream) {
@@ -2085,9 +2102,12 @@ static void run_graphed(opose_ctx* h, const std::string& key, F&& work) {
     }
     // second sighting with nothing reallocated since: capture, instantiate, launch
     OPOSE_HIP_CHECK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    h->capturing = true;
     try {
         work();
+        h->capturing = false;
     } catch (...) {
+        h->capturing = false;
         hipGraph_t g = nullptr;
         (void)hipStreamEndCapture(h->stream, &g);
         if (g) (void)hipGraphDestroy(g);
@@ -2417,6 +2437,19 @@ namespace opose {
 // fn(s) for every scale s, scale s on stream s (0: the handle's stream, others its scale
 // streams), each with workspace slot s; the handle's stream continues after all of them
 static void run_scales_concurrently(opose_ctx* h, int ns, const std::function<void(int)>& fn) {
+    if (h->capturing) {  // one stream while capturing (run_graphed): same work, same slots
+        try {
+            for (int s = ns - 1; s >= 0; --s) {
+                h->slot = s;
+                fn(s);
+            }
+        } catch (...) {
+            h->slot = 0;
+            throw;
+        }
+        h->slot = 0;
+        return;
+    }
     const hipStream_t main = h->stream;
     if (!h->ev_fork) OPOSE_HIP_CHECK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
     OPOSE_HIP_CHECK(hipEventRecord(h->ev_fork, main));

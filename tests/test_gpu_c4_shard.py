@@ -116,7 +116,7 @@ def test_c4_shard_end_to_end_vs_oracle(records, frames_np, f):
     """End to end against the oracle network + post.  On these calibrated crowded frames (~300
     keypoints, ~20 people) the smoothed heat maps have 1-2 px plateaus: any two fp32 evaluations
     of the network put some peaks one pixel apart -- the reference's own torch-CPU network on 8
-    threads and on 1 thread disagree on ~20 % of the keypoint positions.  So the bar is
+    threads and on 1 thread disagree on 12.4 % of the keypoint positions on average.  So the bar is
     set against the float64 network (the exact answer) and relative to the reference's own fp32:
     at most 2 keypoints more than the torch-fp32 network without a float64 keypoint within 1 px
     (a smoothed value within fp32 noise of thre1 may appear or vanish: < 1 % of ~300), no more
