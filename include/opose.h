@@ -159,8 +159,9 @@ int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, i
  * ranks (736x1312 is 53 % of the pyramid's FLOPs; src/body.py:36-50 for one
  * m, cut into output rows).  Every rank of a band group runs the VGG trunk on its band's rows
  * plus a 10-row margin past each cut (recomputed, not exchanged), then the six CPM stages
- * (src/model.py:106-133) on its own rows only.  Before each 3x3 / 7x7 stage layer that needs them, the 3 rows on either side of the
- * band are exchanged with the neighbouring bands: the library packs its top and bottom 3 rows
+ * (src/model.py:106-133) on its own rows only.  Before each 3x3 / 7x7 stage layer that needs
+ * them, the 3 rows on either side of the band are exchanged with the neighbouring bands: the
+ * library packs its top and bottom 3 rows
  * into xbuf's send halves on its stream, calls fn(user, bytes, stream), and unpacks the recv
  * halves.  fn moves send_up to the band above (its recv_dn) and send_dn to the band below (its
  * recv_up), ordered on `stream` (a hipStream_t) or synchronously, and returns 0; it is called
@@ -169,7 +170,7 @@ int opose_body_scale_maps(opose_t* h, const uint8_t* bgr, int N, int H, int W, i
  *         recv_up | recv_dn];  r1 - r0 >= 3;  maps [57, r1-r0, wl] fp32 (host unless
  *         OPOSE_OUT_DEVICE);  bgr one H x W frame (device with OPOSE_IN_DEVICE).
  * Every conv sums each pixel in the order the whole frame's network does (k slabs fixed by the
- * layer and the frame, DESIGN §4.1), so concatenating every band's maps gives
+ * layer and the frame, DESIGN §4.0), so concatenating every band's maps gives
  * opose_body_scale_maps(s) bit for bit. */
 typedef int (*opose_halo_fn)(void* user, size_t bytes, void* stream);
 /* fn == NULL: the library exchanges the halos itself, RCCL send/recv on the handle's stream with

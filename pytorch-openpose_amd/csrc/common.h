@@ -59,7 +59,7 @@ struct ConvArgs {
 //  * padded (X6P, the low-resolution CPM stage buffers): per group one tall image of the N
 //    frames stacked with 3 zero rows above, between and below them and kX6PPad zero units
 //    between consecutive rows (row pitch P = W + kX6PPad, pixel (n, y, x) at row 3 + n*(H+3) + y,
-//    column 3 + x: 3 zero units before a row's pixels, kX6PPad - 3 after them), plus one zero row
+//    column 3 + x: the 3 zero units before a row's pixels also pad the previous row), plus one zero row
 //    at the end: every tap of a 7x7 / 3x3 / 1x1 'same' conv is a constant shift dy*P + dx of the
 //    pixel's unit, and the window of a run of consecutive pixels is contiguous across rows and
 //    frames (conv_win_x6).  fs = (H+3)*P, gs = (N*(H+3)+4)*P, rs = P, o0 = goff*gs + 3*P + 3.  The
@@ -68,11 +68,11 @@ struct X6Layout {
     uint32_t fs, gs, rs, o0;
 };
 
-// Zero units per X6P row: 16, so that P - W is a multiple of 16 units.  A window kernel's B
-// fragment reads 16 consecutive pixels per ds_read_b128 lane group, and a group that crosses a row
-// end then jumps P - W units: a multiple of 16 keeps the 16 units on 16 distinct 16-byte slots of
-// the 256-byte bank row (3 zero units made 2-way conflicts).
-constexpr int kX6PPad = 16;
+// Zero units per X6P row: 3 (the 7x7 taps' reach).  16 (P - W a multiple of 16 units, so a B
+// fragment's 16 pixels stay on 16 distinct LDS bank slots across a row end) cut the modelled
+// bank-conflict cycles of the window kernel's B reads from 51 % to 18.5 % but made every window
+// 30 % longer: the bench's 7x7 launch 0.365 -> 0.376 ms, same box.
+constexpr int kX6PPad = 3;
 __host__ __device__ inline int x6p_pitch(int W) { return W + kX6PPad; }
 
 struct X6Group {

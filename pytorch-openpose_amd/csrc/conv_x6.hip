@@ -8,18 +8,19 @@
 // The dropped terms (a1 b2 + a2 b1 + a2 b2) are below 2^-23 |a b|, the size of one fp32
 // rounding, and every piece product is exact in the fp32 accumulator: the sum carries fp32
 // rounding error like the v_mfma_f32_32x32x2_f32 kernel (tests/test_gpu_x6.py measures both
-// against a float64 reference).  v_mfma_f32_32x32x16_bf16 issues 16x the FLOPs per cycle of
-// the fp32 MFMA, so six of them are 2.7x the fp32 MFMA rate.
+// against a float64 reference).  The bf16 matrix rate is 16x the fp32 MFMA's, so six piece
+// products run at 2.7x the fp32 MFMA rate.
 //
-// * Operand units are 16 bytes = 8 consecutive k of one row (A) / pixel (B): exactly the
-//   per-lane fragment of the 32x32x16 MFMA (lane l: row l&31, k = 8 (l>>5) .. +7), so LDS
-//   tiles are [piece][group][row] unit arrays read with one ds_read_b128 per fragment.
+// * Operand units are 16 bytes = 8 consecutive k of one row (A) / pixel (B): the per-lane
+//   fragment of v_mfma_f32_16x16x32_bf16 (lane l: row / pixel l & 15, k = 8 (l >> 4) .. +7), so
+//   LDS tiles are [piece][group][row] unit arrays read with one ds_read_b128 per fragment.
 // * Both tiles are filled by LDS-DMA: weights (pre-split, [chunk][piece][group][Mpad] units)
-//   by global_load_lds_dwordx4, the im2col pixels of a (piece, channel group, tap) by
+//   by buffer loads to LDS, the im2col pixels of a (piece, channel group, tap) by
 //   buffer_load_dwordx4 ... lds with the zero padding from the buffer range check.
 // * K chunk = 32 k = 4 channel groups of one tap (or 4 taps of a single group when Cin <= 8),
-//   two LDS stages, one barrier per chunk; stream-K ranges, partial slabs and the k-ordered
-//   fixup exactly as conv.hip.
+//   two LDS stages, one barrier per chunk.  Work units (tile, k slab): a tile of a group with
+//   `slabs` slabs sums fixed chunk ranges, each from zero, and conv_x6_fixup folds the slab
+//   partials in slab order (common.h X6Group::slabs, x6.h x6_unit_of).
 // * The epilogue adds bias, applies ReLU and writes the output split again (X6) into a
 //   group slice of a wider buffer (the CPM concat), or fp32 NCHW for the network outputs.
 #include <algorithm>

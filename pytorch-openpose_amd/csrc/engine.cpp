@@ -4,13 +4,11 @@
 //  * topology + state_dict order      src/model.py:25-104 (body), :136-195 (hand)
 //  * Body.__call__ orchestration      src/body.py:24-212
 //  * Hand.__call__ orchestration      src/hand.py:25-75
-// The network runs as ~60 launches of the implicit-GEMM conv kernel (conv.hip); the two
-// CPM branches of a stage share one launch (combined M for their common first conv,
-// two GEMM groups for the rest); stage concatenation is implicit (channel-slice writes).
+// The network runs as one launch per layer of the split-bf16 implicit-GEMM kernels (conv_win.hip,
+// conv_x6.hip, conv1x1_chain.hip; conv.hip is the fp32 alternative): the two CPM branches of a
+// stage and the scales of a pyramid share a launch as groups, each conv sums a pixel in an order
+// fixed by its layer (k slabs, slab_count); stage concatenation is implicit (channel-slice writes).
 #include <dlfcn.h>
-#include <execinfo.h>
-#include <signal.h>
-#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -908,7 +906,7 @@ static int seg_kernel(const opose_ctx* h, const ConvSeg& sg, bool pool) {
     const DevConv* c = sg.c;
     if (!h->win7 || pool || !c->wx6p || !sg.in.padded || (c->ks != 3 && c->ks != 7)) return kKernelX6;
     const long lpix = (long)sg.N * (sg.Hl ? sg.Hl : sg.H) * sg.W;
-    if (c->net == OPOSE_NET_BODY && lpix < 4096 && !getenv("OPOSE_SMALL_WIN")) return kKernelX6;  // TEMP env
+    if (c->net == OPOSE_NET_BODY && lpix < 4096) return kKernelX6;
     if (c->net == OPOSE_NET_HAND && c->ks == 3 && c->lvl == 3) return kKernelX6;
     if (sg.N == 1) return conv_win_fits_rows(sg.W, c->ks) ? kKernelWin : kKernelX6;
     if (conv_win_fits(sg.N, sg.H, sg.W, c->ks)) return kKernelWin;
@@ -951,7 +949,7 @@ static TilePick pick_tile(const std::vector<ColGroup>& cg, bool win, int nK, int
         multi = multi || c.S > 1;
         cols_all += c.cols;
     }
-    const double* ovh = cols_all <= 16384 && !getenv("OPOSE_BIG_TBL") ? kX6OvhSmall : kX6Ovh;  // TEMP env
+    const double* ovh = cols_all <= 16384 ? kX6OvhSmall : kX6Ovh;
     TilePick best;
     for (int ci = 0; ci < 6; ++ci) {
         const int mt = win ? 128 : kX6Cfg[ci][0], pt = win ? 256 : kX6Cfg[ci][1], occ = win ? 1 : kX6Cfg[ci][2];
@@ -1001,11 +999,6 @@ static int slab_count(opose_ctx* h, const DevConv* c, bool win, int N, int H, in
         // the 7x7 stages, and conv5_3_CPM (3x3, 128 outputs: 62 whole tiles for a 368 crop)
         if (!(c->ks == 7 && win) && !(c->ks == 3 && c->Mpad <= 128)) return 1;
         const double T = std::ceil(npix / 256.0) * mr;
-        if (const char* e = getenv("OPOSE_HAND_SLABS")) {  // TEMP sweep
-            int v[7] = {16, 12, 8, 7, 4, 2, 1};
-            sscanf(e, "%d,%d,%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5], &v[6]);
-            return clampS(T < 6 ? v[0] : T < 12 ? v[1] : T < 30 ? v[2] : T < 60 ? v[3] : T < 120 ? v[4] : T < 240 ? v[5] : v[6]);
-        }
         return clampS(T < 6 ? 16 : T < 12 ? 12 : T < 30 ? 8 : T < 60 ? 7 : T < 120 ? 4 : T < 240 ? 2 : 1);
     }
     const int mult = c->pair ? 2 : 1;
@@ -2162,15 +2155,7 @@ void opose_default_params(int net, opose_params* p) {
     p->thre_hand = 0.03;
 }
 
-static void segv_trace(int sig) {
-    void* bt[64];
-    const int n = backtrace(bt, 64);
-    backtrace_symbols_fd(bt, n, 2);
-    signal(sig, SIG_DFL);
-    raise(sig);
-}
 int opose_create(int device, opose_t** out) {
-    if (getenv("OPOSE_SEGV_TRACE")) signal(SIGSEGV, segv_trace);
     if (!out) return OPOSE_E_ARG;
     *out = nullptr;
     auto* h = new opose_ctx();

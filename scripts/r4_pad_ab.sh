@@ -1,0 +1,7 @@
+# same-box A/B of the X6P row pad (alt_lib/pad3.so: 3 zero units, default: 16)
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONDONTWRITEBYTECODE=1
+for r in 1 2; do for v in pad3 pad16; do
+  if [ $v = pad3 ]; then export OPOSE_LIB=alt_lib/pad3.so; else unset OPOSE_LIB; fi
+  timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu --latency-iters 0 > gpurun_out/ab_$v_$r.log 2>&1 || { echo fail; tail -3 gpurun_out/ab_$v_$r.log; exit 1; }
+  echo "$v: $(grep '^{' gpurun_out/ab_$v_$r.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value'],1), d['roofline']['mean_launch_ms'], d['roofline']['frac'])")"
+done; done
