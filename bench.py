@@ -85,6 +85,11 @@ def launch_ranks(args):
 # frames are resident and static for the whole run, so every step may overlap its network with
 # the previous step's post-processing (OPOSE_PIPELINE; BENCH_PIPELINE=0 for the serial A/B)
 PIPELINE = os.environ.get("BENCH_PIPELINE", "1") != "0"
+# BENCH_DEFER=1 (OPOSE_PIPELINE_DEFER): step k's post-processing is enqueued by step k+1 once its
+# network reaches conv3_1, so it overlaps the middle of that network instead of its first layers.
+# Measured same box: 2,065 vs 2,078 frames/s (conv1_2 1.22 -> 0.65 ms, conv3_1 0.30 -> 0.82 ms:
+# the post kernels cost their CU time wherever they overlap), so the default overlaps from the start
+DEFER = PIPELINE and os.environ.get("BENCH_DEFER", "0") != "0"
 
 
 def pmc_traffic():
@@ -379,7 +384,7 @@ def main():
     from src.dist import gather_records
 
     def step():
-        body.infer_records(frames, rec, pipeline=PIPELINE)
+        body.infer_records(frames, rec, pipeline="defer" if DEFER else PIPELINE)
         if world > 1:
             # RCCL all_gather of the per-frame keypoint records, ordered after the library's
             # kernels on its stream (src/dist.py)
@@ -405,6 +410,12 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if DEFER and world > 1:
+        # each step gathered the records complete at that point (the previous step's, deferred):
+        # the last step's post-processing is flushed and gathered here
+        body.handle.flush()
+        with torch.cuda.stream(lib_stream):
+            gather_records(rec, world * B, world)
     body.handle.synchronize()
     torch.cuda.synchronize()
     if world > 1:
@@ -473,7 +484,9 @@ def main():
                                    f"RCCL all_gather of per-frame keypoint records when n_gpus > 1",
                        "frame": [H, W], "frames_per_gpu_per_step": B, "scale_search": [0.5],
                        "net_input": [184, 328], "parallelism": f"frame-sharded dp{world}",
-                       "step_overlap": "network of step k+1 overlaps post-processing of step k (OPOSE_PIPELINE)"
+                       "step_overlap": ("post-processing of step k enqueued by step k+1 once its network reaches "
+                                        "conv3_1 (OPOSE_PIPELINE_DEFER)") if DEFER else
+                                       "network of step k+1 overlaps post-processing of step k (OPOSE_PIPELINE)"
                        if PIPELINE else "none"},
             "frames_total": frames_total,
             "value_host_to_host": h2h_value,

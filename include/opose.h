@@ -62,6 +62,15 @@ enum {
                                 stream and overlaps the previous call's post-network
                                 part; records are still complete in the handle's stream
                                 order. Video-batch throughput mode.                 */
+    OPOSE_PIPELINE_DEFER = 8,/* with OPOSE_PIPELINE: the call's post-network part is
+                                enqueued by the next OPOSE_PIPELINE call once that call's
+                                network has reached its trunk's conv3_1 (so it overlaps
+                                the middle of the next network, not its first layers),
+                                or by opose_flush.  The records are complete in the
+                                handle's stream order only after that; the records and
+                                frames buffers must stay alive until then.  Every other
+                                entry point (and opose_synchronize / opose_signal_stream
+                                / opose_set_stream / opose_destroy) flushes first.  */
 };
 
 #define OPOSE_MAX_SCALES 8
@@ -90,6 +99,9 @@ const char* opose_last_error(const opose_t* h);
 int opose_set_stream(opose_t* h, void* hip_stream);   /* NULL = the handle's own stream */
 void* opose_get_stream(const opose_t* h);
 int opose_synchronize(opose_t* h);
+/* Enqueue a post-network part deferred by OPOSE_PIPELINE_DEFER (no-op otherwise): afterwards the
+ * last call's records are complete in the handle's stream order. */
+int opose_flush(opose_t* h);
 /* Ordering against a caller's stream (e.g. the framework's current stream) for OPOSE_IN_DEVICE /
  * OPOSE_OUT_DEVICE calls.  The reference computes synchronously on one device, so these replace
  * the implicit ordering of its `torch.from_numpy(...).cuda()` / `.cpu()` round trips

@@ -230,6 +230,15 @@ struct ProfAgg {
     double ms = 0, flops = 0, bytes = 0;
 };
 
+// geometry of one pyramid scale (engine.cpp geom)
+struct ScaleGeom {
+    double mult;      // scale * boxsize / H
+    int Hs, Ws;       // cv2.resize output (cvRound(H * mult))
+    int Hp, Wp;       // padded to stride
+    int hl, wl;       // network output
+    double up_sy, up_sx;  // final resize (Hs,Ws) -> (H,W) source steps
+};
+
 }  // namespace
 
 struct GraphEntry {
@@ -350,6 +359,18 @@ struct opose_ctx {
     // `stream` ordered after its own network part.
     hipStream_t nstream = nullptr;
     int nstream_prio = 0;
+    // OPOSE_PIPELINE_DEFER: the last call's post-network part, enqueued by the next pipelined
+    // call after that call's network recorded ev_gate (before its trunk's conv3_1), or by
+    // flush_post.  gate_ev: set while a network part should record the gate.
+    struct DeferredPost {
+        bool pending = false;
+        int N = 0, H = 0, W = 0, set = 0;
+        std::vector<ScaleGeom> gs;
+        opose_params p{};
+        uint8_t* rec = nullptr;
+    } dpost;
+    hipEvent_t ev_gate = nullptr, gate_ev = nullptr;
+    bool gate_done = false;
     hipEvent_t ev_net = nullptr, ev_main = nullptr, ev_post[2] = {nullptr, nullptr};
     // opose_wait_stream / opose_signal_stream / opose_set_stream: ordering against streams the
     // caller owns (a framework's current stream)
@@ -1393,6 +1414,10 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
     for (size_t li = 0; li < vgg.size(); ++li) {
         const Spec& s = vgg[li];
         DevConv* c = find_conv(h, net, s.name);
+        if (h->gate_ev && s.name == "conv3_1") {  // OPOSE_PIPELINE_DEFER: the previous post may start
+            OPOSE_HIP_CHECK(hipEventRecord(h->gate_ev, h->stream));
+            h->gate_done = true;
+        }
         if (li == 0 && s.cin == 3 && s.cout == 64 && s.ks == 3 && s.pad == 1 && vgg.size() > 1 && h->first_direct) {
             DevConv* c2 = find_conv(h, net, vgg[1].name);
             const bool pair12 = conv12_win_ok(vgg[1], c2);
@@ -1819,14 +1844,6 @@ static float* hand_net(opose_ctx* h, const float* x, int N, int Hp, int Wp) {
 }
 
 // ---------------------------------------------------------------- geometry (src/body.py:32-41)
-struct ScaleGeom {
-    double mult;      // scale * boxsize / H
-    int Hs, Ws;       // cv2.resize output (cvRound(H * mult))
-    int Hp, Wp;       // padded to stride
-    int hl, wl;       // network output
-    double up_sy, up_sx;  // final resize (Hs,Ws) -> (H,W) source steps
-};
-
 static int cv_round(double v) { return (int)std::nearbyint(v); }
 
 static ScaleGeom geom(double s, const opose_params& p, int H, int W) {
@@ -1994,8 +2011,10 @@ static int worst_status(const uint8_t* rec, int N, size_t bytes) {
 namespace opose {
 // every entry point that enqueues work on the handle's stream (other than the pipelined body
 // path): select the device, and make the next pipelined network wait for that stream
+static void flush_post(opose_ctx* h);
 static void enter_main(opose_ctx* h) {
     OPOSE_HIP_CHECK(hipSetDevice(h->device));
+    flush_post(h);
     h->main_dirty = true;
 }
 }  // namespace opose
@@ -2172,6 +2191,7 @@ int opose_create(int device, opose_t** out) {
 void opose_destroy(opose_t* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    (void)opose_flush(h);
     (void)hipStreamSynchronize(h->stream);
     delete h;
 }
@@ -2189,6 +2209,7 @@ int opose_set_stream(opose_t* h, void* s) {
     if (!h) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
         OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        flush_post(h);
         const hipStream_t ns = s ? static_cast<hipStream_t>(s) : h->own_stream;
         if (ns != h->stream) {
             // work still queued on the old stream (and on the pipelined network stream) uses the
@@ -2233,6 +2254,7 @@ int opose_signal_stream(opose_t* h, void* s) {
     if (!h) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
         OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        flush_post(h);
         const hipStream_t xs = static_cast<hipStream_t>(s);
         if (xs == h->stream) return OPOSE_OK;
         hipEvent_t e = lazy_event(h->ev_sig);
@@ -2244,9 +2266,19 @@ int opose_signal_stream(opose_t* h, void* s) {
 
 void* opose_get_stream(const opose_t* h) { return h ? h->stream : nullptr; }
 
+int opose_flush(opose_t* h) {
+    if (!h) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        flush_post(h);
+    });
+    return OPOSE_OK;
+}
+
 int opose_synchronize(opose_t* h) {
     if (!h) return OPOSE_E_ARG;
     OPOSE_TRY(h, {
+        flush_post(h);
         OPOSE_HIP_CHECK(hipStreamSynchronize(h->stream));
         if (h->nstream) OPOSE_HIP_CHECK(hipStreamSynchronize(h->nstream));
     });
@@ -2255,6 +2287,7 @@ int opose_synchronize(opose_t* h) {
 
 int opose_set_capacity(opose_t* h, int ppp, int maxp) {
     if (!h || ppp < 1 || maxp < 1 || ppp > 1024 || maxp > 256) return OPOSE_E_ARG;
+    if (opose_flush(h) != OPOSE_OK) return OPOSE_E_HIP;
     h->ppp = ppp;
     h->maxp = maxp;
     return OPOSE_OK;
@@ -2463,8 +2496,33 @@ static void run_scales_concurrently(opose_ctx* h, int ns, const std::function<vo
     for (int s = 1; s < ns; ++s) OPOSE_HIP_CHECK(hipStreamWaitEvent(main, h->ev_join[s], 0));
 }
 
+// the deferred post-network part (OPOSE_PIPELINE_DEFER) on the handle's stream, after `after`
+static void enqueue_deferred_post(opose_ctx* h, hipEvent_t after) {
+    opose_ctx::DeferredPost& d = h->dpost;
+    if (!d.pending) return;
+    d.pending = false;
+    OPOSE_HIP_CHECK(hipStreamWaitEvent(h->stream, after, 0));
+    h->mid_set = d.set;
+    try {
+        body_post_common(h, d.N, d.H, d.W, d.gs, d.p, d.rec);
+    } catch (...) {
+        h->mid_set = 0;
+        throw;
+    }
+    h->mid_set = 0;
+    OPOSE_HIP_CHECK(hipEventRecord(h->ev_post[d.set], h->stream));
+    h->post_pending[d.set] = true;
+}
+
+// enqueue a deferred post-network part now (after its whole network)
+static void flush_post(opose_ctx* h) {
+    if (h->dpost.pending) enqueue_deferred_post(h, h->ev_net);
+}
+
 static void pipelined_body(opose_ctx* h, int N, int H, int W, const std::vector<ScaleGeom>& gs,
-                           const opose_params& p, uint8_t* rec, const std::function<void()>& net_part) {
+                           const opose_params& p, uint8_t* rec, const std::function<void()>& net_part,
+                           bool defer) {
+    if (h->dpost.pending && !(h->dpost.N == N && h->dpost.H == H && h->dpost.W == W)) flush_post(h);
     if (!h->nstream) {
         int lo = 0, hi = 0;
         OPOSE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -2473,7 +2531,7 @@ static void pipelined_body(opose_ctx* h, int N, int H, int W, const std::vector<
         // high / both default measured the same)
         OPOSE_HIP_CHECK(pooled_stream(&h->nstream, hi));
         h->nstream_prio = hi;
-        for (hipEvent_t* e : {&h->ev_net, &h->ev_main, &h->ev_post[0], &h->ev_post[1]})
+        for (hipEvent_t* e : {&h->ev_net, &h->ev_main, &h->ev_post[0], &h->ev_post[1], &h->ev_gate})
             OPOSE_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     const int set = h->next_set;
@@ -2485,18 +2543,41 @@ static void pipelined_body(opose_ctx* h, int N, int H, int W, const std::vector<
         h->main_dirty = false;
     }
     hipStream_t main = h->stream;
+    const bool gate = h->dpost.pending;  // the previous call's post waits for this network's gate
     h->mid_set = set;
     h->stream = h->nstream;
+    h->gate_ev = gate ? h->ev_gate : nullptr;
+    h->gate_done = false;
     try {
         net_part();
+        if (gate && !h->gate_done) OPOSE_HIP_CHECK(hipEventRecord(h->ev_gate, h->nstream));
     } catch (...) {
         h->stream = main;
         h->mid_set = 0;
+        h->gate_ev = nullptr;
         throw;
     }
+    h->gate_ev = nullptr;
     h->stream = main;
+    h->mid_set = 0;
+    // ev_net is re-recorded every call: take the gate first (the deferred post's network ran
+    // before this one on nstream, so the gate implies it)
+    if (gate) enqueue_deferred_post(h, h->ev_gate);
     OPOSE_HIP_CHECK(hipEventRecord(h->ev_net, h->nstream));
+    if (defer) {
+        opose_ctx::DeferredPost& d = h->dpost;
+        d.pending = true;
+        d.N = N;
+        d.H = H;
+        d.W = W;
+        d.set = set;
+        d.gs = gs;
+        d.p = p;
+        d.rec = rec;
+        return;
+    }
     OPOSE_HIP_CHECK(hipStreamWaitEvent(main, h->ev_net, 0));
+    h->mid_set = set;
     body_post_common(h, N, H, W, gs, p, rec);
     OPOSE_HIP_CHECK(hipEventRecord(h->ev_post[set], main));
     h->post_pending[set] = true;
@@ -2544,7 +2625,7 @@ int opose_body_infer(opose_t* h, const uint8_t* bgr, int N, int H, int W, int64_
                 for (int s = 0; s < p.n_scales; ++s) scale_net(s);
         };
         if ((flags & OPOSE_PIPELINE) && (flags & OPOSE_IN_DEVICE) && (flags & OPOSE_OUT_DEVICE)) {
-            pipelined_body(h, N, H, W, gs, p, rec, net_part);
+            pipelined_body(h, N, H, W, gs, p, rec, net_part, (flags & OPOSE_PIPELINE_DEFER) != 0);
         } else if (!lockstep && h->scale_streams && p.n_scales > 1) {  // multi-scale pyramid (C5): scales concurrently
             enter_main(h);
             h->mid_set = 0;

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("OPOSE_LIB", os.path.join(os.path.dirname(_HERE), "lib
 OPOSE_OK = 0
 OPOSE_E_ARG, OPOSE_E_SHAPE, OPOSE_E_HIP, OPOSE_E_WEIGHTS, OPOSE_E_CAPACITY, OPOSE_E_ASSEMBLY = -1, -2, -3, -4, -5, -6
 NET_BODY, NET_HAND = 0, 1
-IN_DEVICE, OUT_DEVICE, PIPELINE = 1, 2, 4
+IN_DEVICE, OUT_DEVICE, PIPELINE, PIPELINE_DEFER = 1, 2, 4, 8
 MAX_SCALES = 8
 
 
@@ -46,6 +46,7 @@ def _load():
         "opose_signal_stream": (I, [P, P]),
         "opose_get_stream": (P, [P]),
         "opose_synchronize": (I, [P]),
+        "opose_flush": (I, [P]),
         "opose_set_capacity": (I, [P, I, I]),
         "opose_body_record_bytes": (S, [P]),
         "opose_load_weights": (I, [P, I, C.POINTER(P), P, I]),
@@ -95,7 +96,7 @@ lib = _load()
 
 EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last_error", "opose_set_stream",
             "opose_wait_stream", "opose_signal_stream",
-            "opose_get_stream", "opose_synchronize", "opose_set_capacity", "opose_body_record_bytes",
+            "opose_get_stream", "opose_synchronize", "opose_flush", "opose_set_capacity", "opose_body_record_bytes",
             "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_hand_forward_pyramid",
             "opose_body_infer",
             "opose_body_post", "opose_body_scale_geom", "opose_body_scale_maps",
@@ -190,6 +191,11 @@ class Handle:
 
     def synchronize(self):
         self.check(lib.opose_synchronize(self.h))
+
+    def flush(self):
+        """Enqueue a post-network part deferred by a pipeline="defer" call (OPOSE_PIPELINE_DEFER):
+        afterwards the last call's records are complete in the handle's stream order."""
+        self.check(lib.opose_flush(self.h))
 
     # ---- RCCL for row-band halo exchanges (opose_body_band_maps with the library's exchange)
     @staticmethod

@@ -239,7 +239,10 @@ class Body(object):
         opose_signal_stream).  pipeline=True
         (OPOSE_PIPELINE, include/opose.h): the frames are complete now and are not modified until
         the handle's stream passes this call; the call's network then overlaps the previous
-        call's post-processing (video-batch throughput)."""
+        call's post-processing (video-batch throughput).  pipeline="defer"
+        (OPOSE_PIPELINE_DEFER): this call's post-processing is enqueued by the next pipelined
+        call once that call's network reaches conv3_1, or by handle.flush() / synchronize() /
+        decode_records(); keep frames and records alive until then."""
         import torch
         N, H, W, _ = frames_dev.shape
         if frames_dev.stride(3) != 1 or frames_dev.stride(2) != 3:
@@ -254,7 +257,8 @@ class Body(object):
         rc = _native.lib.opose_body_infer(self.handle.h, frames_dev.data_ptr(), N, H, W, row_stride,
                                           frame_stride, self.params, records_dev.data_ptr(),
                                           _native.IN_DEVICE | _native.OUT_DEVICE
-                                          | (_native.PIPELINE if pipeline else 0))
+                                          | (_native.PIPELINE if pipeline else 0)
+                                          | (_native.PIPELINE_DEFER if pipeline == "defer" else 0))
         self.handle.check(rc)
         if pipeline:
             # outputs stay in the handle's stream order (torch's stream must not wait for them, or

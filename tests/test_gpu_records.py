@@ -69,6 +69,31 @@ def test_records_pipelined(body, batches, expected):
         assert np.array_equal(c, ec) and np.array_equal(s, es)
 
 
+@pytest.mark.parametrize("mix", ["defer_only", "mixed"])
+def test_records_pipelined_deferred(body, batches, expected, mix):
+    """pipeline="defer" (OPOSE_PIPELINE_DEFER, bench.py's default): each call's post-processing
+    is enqueued by the next call once its network reaches conv3_1 (or by flush / synchronize /
+    decode_records / any other entry point).  Every record equals the host path's, whether the
+    deferred calls run back to back, alternate with plain pipelined calls, or are followed by a
+    host-path call, a decode without an explicit flush, or a synchronize."""
+    dev = [torch.from_numpy(f).cuda() for f in batches]
+    torch.cuda.synchronize()
+    order = [0, 1, 2, 0, 2, 1, 1]
+    for _ in range(8):
+        modes = ["defer" if (mix == "defer_only" or k % 2 == 0) else True for k in range(len(order))]
+        recs = [body.infer_records(dev[i], pipeline=m) for i, m in zip(order, modes)]
+        body.handle.synchronize()
+        for i, rec in zip(order, recs):
+            _check(body, rec, expected[i])
+    r0 = body.infer_records(dev[1], pipeline="defer")
+    mid = body.batch(batches[2])  # another entry point flushes the deferred post first
+    r1 = body.infer_records(dev[0], pipeline="defer")
+    _check(body, r0, expected[1])
+    _check(body, r1, expected[0])  # decode_records flushes
+    for (c, s), (ec, es) in zip(mid, expected[2]):
+        assert np.array_equal(c, ec) and np.array_equal(s, es)
+
+
 def test_bench_frame_post_exact_vs_oracle(body):
     """The bench's own configuration: a uniform-random 368x656 frame at scale 0.5 with the bench's
     calibrated weights (crowded: ~300 peaks and ~20 people per frame).  The device path bench.py
