@@ -656,73 +656,76 @@ __device__ __forceinline__ float x8_at(const float* __restrict__ low, int hl, in
     return cubic_sample_f32(low, wl, cubic_tap(y8, 0.125, hl), cubic_tap(x8, 0.125, wl));
 }
 
-__device__ __forceinline__ float pick5(const float (&p)[5], int d) {
-    float v = p[0];
-    v = d == 1 ? p[1] : v;
-    v = d == 2 ? p[2] : v;
-    v = d == 3 ? p[3] : v;
-    v = d == 4 ? p[4] : v;
-    return v;
+// source floor of cubic_tap (its taps are floor - 1 .. floor + 2, clamped)
+__device__ __forceinline__ int cubic_floor(int d, double scale) {
+    return (int)floorf((float)(((double)d + 0.5) * scale - 0.5));
 }
 
 // the final resize (taps ty / tx over the x8 map) at one point of the PAF pair (chx, chx + 1), the
-// x8 values evaluated from the low-res planes lx / ly.  The 4 x 4 x8 samples read a 5 x 5 low-res
-// patch (the taps of a cubic resize are 4 consecutive indices; 4 consecutive x8 rows or columns
-// span 3/8 of a low-res step, so their 4-tap supports fall in 5 consecutive low-res rows /
-// columns), so the patch is loaded once and every horizontal sum computed once per (patch row, x8
-// column).  Each value is cubic_resize_rows<0>'s sum, then cubic_sample_f32's over those, in the
-// same order: bit-identical to resampling the staged x8 map.
+// x8 values evaluated from the low-res planes lx / ly.  The 4 x 4 x8 samples read a 5 x 5
+// low-res patch: 4 consecutive x8 rows (columns) have source floors f0 or f0 + 1, so tap m of x8
+// row r is patch row (f_r - f0) + m of the patch whose row k holds low-res row clamp(f0 - 1 + k)
+// -- the clamped tap's row.  The patch is loaded once, every horizontal sum computed once per
+// (patch row, x8 column), and each value is cubic_resize_rows<0>'s sum, then cubic_sample_f32's
+// over those, in their order: bit-identical to resampling the staged x8 map.
 __device__ __forceinline__ void resize_x8_pair(const float* __restrict__ lx, const float* __restrict__ ly, int hl,
                                                int wl, const CubicTap& ty, const CubicTap& tx, float& ox, float& oy) {
-    CubicTap cx[4], ry[4];
+    float cxc[4][4];  // the x8 columns' horizontal coefficients
+    bool bx[4], by[4];  // x8 column / row j's floor is f0 + 1
+    const int fx0 = cubic_floor(tx.i[0], 0.125), fy0 = cubic_floor(ty.i[0], 0.125);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        cx[j] = cubic_tap(tx.i[j], 0.125, wl);
-        ry[j] = cubic_tap(ty.i[j], 0.125, hl);
-    }
-    const int r0 = ry[0].i[0], c0 = cx[0].i[0];
+        const CubicTap t = cubic_tap(tx.i[j], 0.125, wl);
 #pragma unroll
-    for (int ch = 0; ch < 2; ++ch) {
+        for (int n = 0; n < 4; ++n) cxc[j][n] = t.c[n];
+        bx[j] = cubic_floor(tx.i[j], 0.125) != fx0;
+        by[j] = cubic_floor(ty.i[j], 0.125) != fy0;
+    }
+    int cc[5];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) cc[d] = min(max(fx0 - 1 + d, 0), wl - 1);
+#pragma unroll 1
+    for (int ch = 0; ch < 2; ++ch) {  // one channel at a time: half the live registers
         const float* plane = ch ? ly : lx;
-        float hsum[4][5];  // [x8 column j][patch row k]
+        float hs[4][5];  // [x8 column j][patch row k]
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
-            const float* row = plane + (size_t)min(r0 + k, hl - 1) * wl;
+            const float* row = plane + (size_t)min(max(fy0 - 1 + k, 0), hl - 1) * wl;
             float p[5];
 #pragma unroll
-            for (int d = 0; d < 5; ++d) p[d] = row[min(c0 + d, wl - 1)];
+            for (int d = 0; d < 5; ++d) p[d] = row[cc[d]];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                float v = pick5(p, cx[j].i[0] - c0) * cx[j].c[0];
-                v = v + pick5(p, cx[j].i[1] - c0) * cx[j].c[1];
-                v = v + pick5(p, cx[j].i[2] - c0) * cx[j].c[2];
-                v = v + pick5(p, cx[j].i[3] - c0) * cx[j].c[3];
-                hsum[j][k] = v;
+                const bool b = bx[j];
+                float v = (b ? p[1] : p[0]) * cxc[j][0];
+                v = v + (b ? p[2] : p[1]) * cxc[j][1];
+                v = v + (b ? p[3] : p[2]) * cxc[j][2];
+                v = v + (b ? p[4] : p[3]) * cxc[j][3];
+                hs[j][k] = v;
             }
         }
-        float h[4];
+        float o = 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+            const CubicTap ry = cubic_tap(ty.i[r], 0.125, hl);  // the x8 row's vertical coefficients
+            const bool b = by[r];
             float x8[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                float o = pick5(hsum[j], ry[r].i[0] - r0) * ry[r].c[0];
-                o = o + pick5(hsum[j], ry[r].i[1] - r0) * ry[r].c[1];
-                o = o + pick5(hsum[j], ry[r].i[2] - r0) * ry[r].c[2];
-                o = o + pick5(hsum[j], ry[r].i[3] - r0) * ry[r].c[3];
-                x8[j] = o;
+                float u = (b ? hs[j][1] : hs[j][0]) * ry.c[0];
+                u = u + (b ? hs[j][2] : hs[j][1]) * ry.c[1];
+                u = u + (b ? hs[j][3] : hs[j][2]) * ry.c[2];
+                u = u + (b ? hs[j][4] : hs[j][3]) * ry.c[3];
+                x8[j] = u;
             }
             float v = x8[0] * tx.c[0];
             v = v + x8[1] * tx.c[1];
             v = v + x8[2] * tx.c[2];
             v = v + x8[3] * tx.c[3];
-            h[r] = v;
+            o = r == 0 ? v * ty.c[0] : o + v * ty.c[r];
         }
-        float o = h[0] * ty.c[0];
-        o = o + h[1] * ty.c[1];
-        o = o + h[2] * ty.c[2];
-        o = o + h[3] * ty.c[3];
-        (ch ? oy : ox) = o;
+        if (ch) oy = o;
+        else ox = o;
     }
 }
 
