@@ -971,11 +971,16 @@ static TilePick pick_tile(const std::vector<ColGroup>& cg, bool win, int nK, int
         cols_all += c.cols;
     }
     const double* ovh = cols_all <= 16384 ? kX6OvhSmall : kX6Ovh;
+    // launches of one small frame's layers (C2: at most 4,096 columns per group): 128 x 64 tiles,
+    // one work unit per workgroup slot (slab_count) -- the measured best of 128 x 64 / 128 x 128 /
+    // 64 x 128 / 64 x 64 / 128 x 256 at 6-32 slabs on C2's 7x7 layers (round 4 sweep)
+    const bool small1 = !win && cols_all <= 4096L * (long)cg.size() && Mpad % 128 == 0 && multi;
     TilePick best;
     for (int ci = 0; ci < 6; ++ci) {
         const int mt = win ? 128 : kX6Cfg[ci][0], pt = win ? 256 : kX6Cfg[ci][1], occ = win ? 1 : kX6Cfg[ci][2];
         if (win && ci > 0) break;
         if (Mpad % mt) continue;
+        if (small1 && (mt != 128 || pt != 64)) continue;
         const std::vector<SlabGroup> gs = slab_groups(cg, Mpad, mt, pt);
         long units = 0, tiles = 0;
         for (const SlabGroup& g : gs) {
@@ -1024,6 +1029,14 @@ static int slab_count(opose_ctx* h, const DevConv* c, bool win, int N, int H, in
     }
     const int mult = c->pair ? 2 : 1;
     if (std::ceil(npix / 256.0) * mr * mult >= 160) return 1;  // the bench's batches: whole tiles fill the chip
+    if (!win && npix <= 4096 && c->Mpad % 128 == 0) {
+        // one small frame (C2 and the pyramid's small scales on conv_x6): 128 x 64 tiles (pick_tile),
+        // as many slabs as keep (tiles x slabs) within the 512 workgroup slots (two per CU) -- one
+        // unit per workgroup.  C2's 7x7 layers: 10 slabs (300 units) 35.4 us, 16 (480) 33.6 us,
+        // 20-32 (several units per workgroup) 40-43 us
+        const long tiles = (long)(c->Mpad / 128) * ((npix + 63) / 64) * mult;
+        return clampS(std::max<long>(1, 512 / tiles));
+    }
     // otherwise the count that prices lowest for the segment run alone (with its CPM sibling), as
     // Body(frame) runs a scale -- plus, for one frame whose H/8 map has >= 40 rows (a scale the
     // balanced C5 split may cut into row bands, src/dist.py split_plan), the same layer on a fifth
@@ -1211,7 +1224,21 @@ struct ChainSeg {
 // with OPOSE_FUSE_1X1=0 or a shape the kernel does not take, the two convs as separate launches
 // through `mid`.
 static void run_chain_x6(opose_ctx* h, const std::vector<ChainSeg>& segs) {
-    bool fuse = h->fuse1x1 && !segs.empty() && segs.size() <= (size_t)kX6Groups;
+    // a small frame's 512-wide stage-1 pair (C2: 943 pixels, 15 workgroups of 64 pixels per
+    // branch in the fused kernel, 42 us) runs as two launches over 128 x 64 tiles: the same sums
+    // (1x1 convs never split k, the fused kernel rounds the intermediate like conv_x6's epilogue)
+    {
+        std::vector<ChainSeg> small, rest;
+        for (const ChainSeg& sg : segs)
+            ((long)sg.N * (sg.Hl ? sg.Hl : sg.H) * sg.W <= 4096 && sg.c1->cout >= 256 ? small : rest).push_back(sg);
+        if (!small.empty() && !rest.empty()) {
+            run_chain_x6(h, small);
+            run_chain_x6(h, rest);
+            return;
+        }
+    }
+    bool fuse = h->fuse1x1 && !segs.empty() && segs.size() <= (size_t)kX6Groups &&
+                !((long)segs[0].N * (segs[0].Hl ? segs[0].Hl : segs[0].H) * segs[0].W <= 4096 && segs[0].c1->cout >= 256);
     for (const ChainSeg& sg : segs) {
         const DevConv *c1 = sg.c1, *c2 = sg.c2;
         fuse = fuse && c1->ks == 1 && c2->ks == 1 && c1->cin_g == 16 && c1->cout == c1->Mpad && c1->Mpad % 128 == 0 &&

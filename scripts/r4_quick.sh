@@ -1,4 +1,3 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_records.py tests/test_gpu_c4_shard.py tests/test_gpu_scale_shard.py tests/test_gpu_fullsize.py > gpurun_out/q_tests.log 2>&1 || { grep -E "FAIL|Error|assert" gpurun_out/q_tests.log | head; tail -3 gpurun_out/q_tests.log; exit 1; }
-tail -1 gpurun_out/q_tests.log
-BENCH_PIPELINE=0 timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu --latency-iters 0 > gpurun_out/q_serial.log 2>&1 && grep '^{' gpurun_out/q_serial.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], {k: d['stage_ms_per_step'][k] for k in ('paf_score','upsample8','gauss_nms_resize','assemble','limb_greedy')})"
+timeout -k 10 120 python scripts/c2_profile.py > gpurun_out/q_c2.log 2>&1 && grep -v amdgpu gpurun_out/q_c2.log | head -14 | cut -c1-150 &&
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_x6.py tests/test_gpu_parity.py tests/test_gpu_scale_shard.py tests/test_gpu_records.py > gpurun_out/q_tests.log 2>&1; rc=$?; tail -1 gpurun_out/q_tests.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" gpurun_out/q_tests.log | head; exit 1; }
