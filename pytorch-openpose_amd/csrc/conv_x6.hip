@@ -380,7 +380,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_x6(X6Args a) {
             if (a.pool) {
                 // 2x2 max over the quad's 4 lanes, then bias + ReLU (both monotone: identical to
                 // pooling the biased, rectified values), one lane per quad stores the pooled pixel.
-                // Whole tiles only (the host runs pooled convs data parallel), X6 output.
+                // X6 output; the slabs of a multi-slab pooled tile are pooled by conv_x6_fixup.
                 const int q = p >> 2;
                 const int n = q / HWo;
                 const int remo = q - n * HWo;
@@ -486,39 +486,67 @@ __global__ __launch_bounds__(256) void conv_x6_fixup(X6Args a) {
     if (p >= G.npix) return;
     const int cout8 = (G.cout + 7) & ~7;
     if (mg >= (G.out_f32 ? G.cout : cout8)) return;
-    // the unit's two channel quads (x6.h slab layout): quads ml0/4 and ml0/4 + 1 of pixel pl
-    auto slab = [&](int w) __attribute__((always_inline)) {
-        return reinterpret_cast<const f32x4*>(a.partial + (size_t)w * (MT * PT)) + (size_t)(ml0 / 4) * PT + pl;
+    // the unit's two channel quads (x6.h slab layout): quads ml0/4 and ml0/4 + 1 of column c
+    auto slab = [&](int w, int c) __attribute__((always_inline)) {
+        return reinterpret_cast<const f32x4*>(a.partial + (size_t)w * (MT * PT)) + (size_t)(ml0 / 4) * PT + c;
+    };
+    // column c's 8 sums, slab partials folded in slab order
+    auto fold = [&](int c, float (&v)[8]) __attribute__((always_inline)) {
+        {
+            const f32x4* s = slab(w0, c);
+            const f32x4 lo = s[0], hi = s[PT];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                v[t] = lo[t];
+                v[4 + t] = hi[t];
+            }
+        }
+        int w = w0 + 1;
+        for (; w < w1; w += 2) {
+            const f32x4 *s0 = slab(w, c), *s1 = slab(w + 1, c);
+            const f32x4 a0 = s0[0], a1 = s0[PT], b0 = s1[0], b1 = s1[PT];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                v[t] = (v[t] + a0[t]) + b0[t];
+                v[4 + t] = (v[4 + t] + a1[t]) + b1[t];
+            }
+        }
+        if (w == w1) {
+            const f32x4* s = slab(w, c);
+            const f32x4 lo = s[0], hi = s[PT];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                v[t] += lo[t];
+                v[4 + t] += hi[t];
+            }
+        }
     };
     float v[8];
-    {
-        const f32x4* s = slab(w0);
-        const f32x4 lo = s[0], hi = s[PT];
+    if (a.pool) {
+        // pooled conv (columns quad-major, the conv's pooled epilogue): the quad's lead thread folds
+        // its 4 columns, takes their max, then bias + ReLU, and stores the pooled unit
+        if (pl & 3) return;
+        fold(pl, v);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            v[t] = lo[t];
-            v[4 + t] = hi[t];
-        }
-    }
-    int w = w0 + 1;
-    for (; w < w1; w += 2) {
-        const f32x4 *s0 = slab(w), *s1 = slab(w + 1);
-        const f32x4 a0 = s0[0], a1 = s0[PT], b0 = s1[0], b1 = s1[PT];
+        for (int c = 1; c < 4; ++c) {
+            float u[8];
+            fold(pl + c, u);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            v[t] = (v[t] + a0[t]) + b0[t];
-            v[4 + t] = (v[4 + t] + a1[t]) + b1[t];
+            for (int t = 0; t < 8; ++t) v[t] = fmaxf(v[t], u[t]);
         }
-    }
-    if (w == w1) {
-        const f32x4* s = slab(w);
-        const f32x4 lo = s[0], hi = s[PT];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            v[t] += lo[t];
-            v[4 + t] += hi[t];
+        for (int t = 0; t < 8; ++t) {
+            const int m = mg + t;
+            v[t] += m < G.cout ? G.bias[m] : 0.f;
+            if (G.relu) v[t] = fmaxf(v[t], 0.f);
         }
+        const int Wo = G.W / 2, HWo = (G.H / 2) * Wo;
+        const int q = p >> 2, n = q / HWo, remo = q - n * HWo;
+        const int yo = remo / Wo, xo = remo - yo * Wo;
+        store8_x6(static_cast<uint8_t*>(G.out) + (size_t)x6_unit(G.out_l, n, mg >> 3, yo, xo) * 16, G.out_ps, v);
+        return;
     }
+    fold(pl, v);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         const int m = mg + t;
@@ -781,7 +809,7 @@ X6Args x6_number_tiles(const X6Args& a0, int mt, int pt) {
         X6Group& G = a.g[g];
         if (G.npix <= 0) throw std::invalid_argument("conv_x6: empty group");
         if (G.slabs < 1) G.slabs = 1;
-        if (G.slabs > a.nK || (a.pool && G.slabs != 1)) throw std::invalid_argument("conv_x6: bad slab count");
+        if (G.slabs > a.nK) throw std::invalid_argument("conv_x6: bad slab count");
         const int tg = (a.Mpad / mt) * ((G.npix + pt - 1) / pt);
         G.t0 = t;
         G.u0 = u;

@@ -971,10 +971,10 @@ static TilePick pick_tile(const std::vector<ColGroup>& cg, bool win, int nK, int
         cols_all += c.cols;
     }
     const double* ovh = cols_all <= 16384 ? kX6OvhSmall : kX6Ovh;
-    // launches of one small frame's layers (C2: at most 4,096 columns per group): 128 x 64 tiles,
+    // multi-slab launches of one small frame's layers (C2; slab_count's small-frame rule): 128 x 64 tiles,
     // one work unit per workgroup slot (slab_count) -- the measured best of 128 x 64 / 128 x 128 /
     // 64 x 128 / 64 x 64 / 128 x 256 at 6-32 slabs on C2's 7x7 layers (round 4 sweep)
-    const bool small1 = !win && cols_all <= 4096L * (long)cg.size() && Mpad % 128 == 0 && multi;
+    const bool small1 = !win && cols_all <= 16384L * (long)cg.size() && Mpad % 128 == 0 && multi;
     TilePick best;
     for (int ci = 0; ci < 6; ++ci) {
         const int mt = win ? 128 : kX6Cfg[ci][0], pt = win ? 256 : kX6Cfg[ci][1], occ = win ? 1 : kX6Cfg[ci][2];
@@ -1016,12 +1016,13 @@ static TilePick pick_tile(const std::vector<ColGroup>& cg, bool win, int nK, int
 // units pack evenly over 256 workgroups (longest-first, lpt_units).
 static int slab_count(opose_ctx* h, const DevConv* c, bool win, int N, int H, int W, bool pool) {
     const int nK = win ? c->nK6p : c->nK6;
-    if (pool || c->ks == 1 || nK < 8) return 1;  // 1x1: the closing pairs' unfused form sums like the fused chain
+    if (c->ks == 1 || nK < 8) return 1;  // 1x1: the closing pairs' unfused form sums like the fused chain
     const int smax = nK / 4;
     const long npix = (long)N * H * W;
     const double mr = c->Mpad / 128.0;
     auto clampS = [&](long s) { return (int)std::max<long>(1, std::min<long>(s, smax)); };
     if (c->net == OPOSE_NET_HAND) {
+        if (pool) return 1;
         // the 7x7 stages, and conv5_3_CPM (3x3, 128 outputs: 62 whole tiles for a 368 crop)
         if (!(c->ks == 7 && win) && !(c->ks == 3 && c->Mpad <= 128)) return 1;
         const double T = std::ceil(npix / 256.0) * mr;
@@ -1029,14 +1030,16 @@ static int slab_count(opose_ctx* h, const DevConv* c, bool win, int N, int H, in
     }
     const int mult = c->pair ? 2 : 1;
     if (std::ceil(npix / 256.0) * mr * mult >= 160) return 1;  // the bench's batches: whole tiles fill the chip
-    if (!win && npix <= 4096 && c->Mpad % 128 == 0) {
+    if (!win && npix <= (pool ? 16384 : 4096) && c->Mpad % 128 == 0) {
         // one small frame (C2 and the pyramid's small scales on conv_x6): 128 x 64 tiles (pick_tile),
         // as many slabs as keep (tiles x slabs) within the 512 workgroup slots (two per CU) -- one
         // unit per workgroup.  C2's 7x7 layers: 10 slabs (300 units) 35.4 us, 16 (480) 33.6 us,
         // 20-32 (several units per workgroup) 40-43 us
+        // (pooled convs: conv_x6_fixup pools the folded quads)
         const long tiles = (long)(c->Mpad / 128) * ((npix + 63) / 64) * mult;
         return clampS(std::max<long>(1, 512 / tiles));
     }
+    if (pool) return 1;
     // otherwise the count that prices lowest for the segment run alone (with its CPM sibling), as
     // Body(frame) runs a scale -- plus, for one frame whose H/8 map has >= 40 rows (a scale the
     // balanced C5 split may cut into row bands, src/dist.py split_plan), the same layer on a fifth
