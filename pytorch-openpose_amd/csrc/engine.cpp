@@ -963,7 +963,8 @@ struct TilePick {
     int mt = 0, pt = 0, grid = 0;
     double cost = 1e300;
 };
-static TilePick pick_tile(const std::vector<ColGroup>& cg, bool win, int nK, int Mpad) {
+static TilePick pick_tile(const std::vector<ColGroup>& cg, bool win, int nK, int Mpad, bool pool = false,
+                          bool small_tiles = true) {
     bool multi = false;
     long cols_all = 0;
     for (const ColGroup& c : cg) {
@@ -974,7 +975,8 @@ static TilePick pick_tile(const std::vector<ColGroup>& cg, bool win, int nK, int
     // multi-slab launches of one small frame's layers (C2; slab_count's small-frame rule): 128 x 64 tiles,
     // one work unit per workgroup slot (slab_count) -- the measured best of 128 x 64 / 128 x 128 /
     // 64 x 128 / 64 x 64 / 128 x 256 at 6-32 slabs on C2's 7x7 layers (round 4 sweep)
-    const bool small1 = !win && cols_all <= 16384L * (long)cg.size() && Mpad % 128 == 0 && multi;
+    const bool small1 =
+        small_tiles && !win && cols_all <= (pool ? 16384L : 4096L) * (long)cg.size() && Mpad % 128 == 0 && multi;
     TilePick best;
     for (int ci = 0; ci < 6; ++ci) {
         const int mt = win ? 128 : kX6Cfg[ci][0], pt = win ? 256 : kX6Cfg[ci][1], occ = win ? 1 : kX6Cfg[ci][2];
@@ -1059,7 +1061,8 @@ static int slab_count(opose_ctx* h, const DevConv* c, bool win, int N, int H, in
     for (int S : cand) {
         if (S > std::max(1, smax)) break;
         double cost = pick_tile(std::vector<ColGroup>(mult, ColGroup{npix, S}), win, nK, c->Mpad).cost;
-        if (bpix) cost += pick_tile(std::vector<ColGroup>(mult, ColGroup{bpix, S}), win, nK, c->Mpad).cost;
+        // (the band proxy is a slice of a large scale: any tile, not the small-frame rule's)
+        if (bpix) cost += pick_tile(std::vector<ColGroup>(mult, ColGroup{bpix, S}), win, nK, c->Mpad, false, false).cost;
         if (cost < best_cost * 0.97) {
             best_cost = cost;
             best = S;
@@ -1085,7 +1088,7 @@ static opose_ctx::ConvPlan plan_launch(opose_ctx* h, const std::vector<ConvSeg>&
         cg.push_back({pool ? (long)s.N * (s.H / 2) * (s.W / 2) * 4 : (long)s.N * s.H * s.W, s.slabs});
         multi = multi || s.slabs > 1;
     }
-    const TilePick tp = pick_tile(cg, win, nK, Mpad);
+    const TilePick tp = pick_tile(cg, win, nK, Mpad, pool);
     opose_ctx::ConvPlan best;
     best.mt = tp.mt;
     best.pt = tp.pt;
