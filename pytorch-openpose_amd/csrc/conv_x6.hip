@@ -877,11 +877,23 @@ void launch_from_x6(const uint8_t* in, int cg, int goff, uint32_t ps, int C, int
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 // F32OUT: the 64 channels as fp32 units of 8 channels (32 bytes, [N][8][H*W] units) for
 // conv3_pool_win_x6<true>, which splits them itself: 256 instead of 384 bytes per pixel.
+// segment of a multi-segment launch owning block (or tile) b: the last one whose b0 <= b
+__device__ __forceinline__ int conv1_seg_of(const Conv1Segs& S, int b) {
+    int k = 0;
+    while (k + 1 < S.n && b >= S.s[k + 1].b0) ++k;
+    return k;
+}
+
 template <int CIN, bool F32OUT>
-__global__ __launch_bounds__(256) void conv_first_x6_kernel(const float* __restrict__ x, int N, int H, int W,
-                                                            const float* __restrict__ wt, int Mpad,
-                                                            const float* __restrict__ bias, uint8_t* __restrict__ out,
-                                                            uint32_t ops) {
+__global__ __launch_bounds__(256) void conv_first_x6_kernel(Conv1Segs S, const float* __restrict__ wt, int Mpad,
+                                                            const float* __restrict__ bias) {
+    const int sk = conv1_seg_of(S, blockIdx.x);  // this block's segment (a pyramid scale)
+    const float* __restrict__ x = static_cast<const float*>(S.s[sk].in);
+    const int N = S.s[sk].N, H = S.s[sk].H, W = S.s[sk].W;
+    uint8_t* __restrict__ out = S.s[sk].out;
+    const uint32_t ops = S.s[sk].ops;
+    const int lblock = blockIdx.x - S.s[sk].b0;
+    const int lgrid = (sk + 1 < S.n ? S.s[sk + 1].b0 : (int)gridDim.x) - S.s[sk].b0;
     // weights (K x 64, K order (channel, tap)) and bias staged once per workgroup: the inner loop
     // reads them as LDS broadcasts instead of waiting on a global load per tap (0.395 -> 0.338 ms
     // per 32-frame step; two pixels per thread made the compiler hold a group's 54 weight reads
@@ -894,7 +906,7 @@ __global__ __launch_bounds__(256) void conv_first_x6_kernel(const float* __restr
     __syncthreads();
     const int HW = H * W;
     const size_t total = (size_t)N * HW;
-    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    for (size_t e = (size_t)lblock * blockDim.x + threadIdx.x; e < total; e += (size_t)lgrid * blockDim.x) {
         const int n = (int)(e / HW);
         const int r = (int)(e - (size_t)n * HW);
         const int y = r / W, xx = r - (r / W) * W;
@@ -949,16 +961,27 @@ __global__ __launch_bounds__(256) void conv_first_x6_kernel(const float* __restr
     }
 }
 
+void launch_conv_first_x6_segs(Conv1Segs S, const float* wt, int Mpad, const float* bias, bool f32_out,
+                               hipStream_t st) {
+    if (S.n < 1 || S.n > kConv1Segs) throw std::invalid_argument("conv_first_x6: segment count");
+    int grid = 0;
+    for (int k = 0; k < S.n; ++k) {
+        S.s[k].b0 = grid;
+        grid += grid_for((size_t)S.s[k].N * S.s[k].H * S.s[k].W);
+    }
+    if (f32_out)
+        hipLaunchKernelGGL((conv_first_x6_kernel<3, true>), dim3(grid), dim3(256), 0, st, S, wt, Mpad, bias);
+    else
+        hipLaunchKernelGGL((conv_first_x6_kernel<3, false>), dim3(grid), dim3(256), 0, st, S, wt, Mpad, bias);
+}
+
 void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const float* wt, int Mpad, const float* bias,
                           uint8_t* out, uint32_t ops, bool f32_out, hipStream_t st) {
     if (Cin != 3) throw std::invalid_argument("conv_first_x6: Cin must be 3");
-    const int grid = grid_for((size_t)N * H * W);
-    if (f32_out)
-        hipLaunchKernelGGL((conv_first_x6_kernel<3, true>), dim3(grid), dim3(256), 0, st, x, N, H, W, wt, Mpad, bias,
-                           out, ops);
-    else
-        hipLaunchKernelGGL((conv_first_x6_kernel<3, false>), dim3(grid), dim3(256), 0, st, x, N, H, W, wt, Mpad, bias,
-                           out, ops);
+    Conv1Segs S{};
+    S.n = 1;
+    S.s[0] = Conv1Seg{x, out, 0u, ops, N, H, W, 0};
+    launch_conv_first_x6_segs(S, wt, Mpad, bias, f32_out, st);
 }
 
 // ---------------------------------------------------------------- windowed conv1_2 (+ pool)
@@ -1004,20 +1027,26 @@ struct WinSmem {
 // the same LDS window (block 1's when every wave is past block 0's reads; the other workgroup on
 // the CU covers the load latency).
 template <bool F32IN>
-__global__ __launch_bounds__(256, 2) void conv3_pool_win_x6_kernel(const uint8_t* __restrict__ in, uint32_t ips,
-                                                                   int N, int H, int W,
-                                                                   const uint8_t* __restrict__ wt,
-                                                                   const float* __restrict__ bias,
-                                                                   uint8_t* __restrict__ out, uint32_t ops) {
+__global__ __launch_bounds__(256, 2) void conv3_pool_win_x6_kernel(Conv1Segs S, const uint8_t* __restrict__ wt,
+                                                                   const float* __restrict__ bias) {
     __shared__ WinSmem sm;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ntx = (W + V_TW - 1) / V_TW, nty = (H + V_TH - 1) / V_TH;
-    int n, y0, x0;
+    int t;
     {
         const int Gw = gridDim.x, b = blockIdx.x;
         const int q = Gw >> 3, rr = Gw & 7, xcd = b & 7;
-        const int t = xcd * q + min(xcd, rr) + (b >> 3);  // XCD-contiguous tiles (guide T1)
+        t = xcd * q + min(xcd, rr) + (b >> 3);  // XCD-contiguous tiles (guide T1)
+    }
+    const int sk = conv1_seg_of(S, t);  // the tile's segment (a pyramid scale)
+    const uint8_t* __restrict__ in = static_cast<const uint8_t*>(S.s[sk].in);
+    uint8_t* __restrict__ out = S.s[sk].out;
+    const uint32_t ips = S.s[sk].ips, ops = S.s[sk].ops;
+    const int H = S.s[sk].H, W = S.s[sk].W;
+    t -= S.s[sk].b0;
+    const int ntx = (W + V_TW - 1) / V_TW, nty = (H + V_TH - 1) / V_TH;
+    int n, y0, x0;
+    {
         const int tx = t % ntx, rest = t / ntx;
         x0 = tx * V_TW;
         y0 = (rest % nty) * V_TH;
@@ -1239,17 +1268,28 @@ __global__ __launch_bounds__(256, 2) void conv3_pool_win_x6_kernel(const uint8_t
     }
 }
 
+void launch_conv3_pool_win_x6_segs(Conv1Segs S, const uint8_t* wt, const float* bias, bool f32_in, hipStream_t st) {
+    if (S.n < 1 || S.n > kConv1Segs) throw std::invalid_argument("conv3_pool_win_x6: segment count");
+    int tiles = 0;
+    for (int k = 0; k < S.n; ++k) {
+        const Conv1Seg& g = S.s[k];
+        if (g.H < 2 || g.W < 2 || (size_t)g.N * 8 * g.H * g.W * 16 >= 0x80000000ull)
+            throw std::invalid_argument("conv3_pool_win_x6: frame shape out of range");
+        S.s[k].b0 = tiles;
+        tiles += g.N * ((g.H + V_TH - 1) / V_TH) * ((g.W + V_TW - 1) / V_TW);
+    }
+    if (f32_in)
+        hipLaunchKernelGGL(conv3_pool_win_x6_kernel<true>, dim3(tiles), dim3(64 * V_NW), 0, st, S, wt, bias);
+    else
+        hipLaunchKernelGGL(conv3_pool_win_x6_kernel<false>, dim3(tiles), dim3(64 * V_NW), 0, st, S, wt, bias);
+}
+
 void launch_conv3_pool_win_x6(const uint8_t* in, uint32_t ips, int N, int H, int W, const uint8_t* wt,
                               const float* bias, uint8_t* out, uint32_t ops, bool f32_in, hipStream_t st) {
-    if (H < 2 || W < 2 || (size_t)N * 8 * H * W * 16 >= 0x80000000ull)
-        throw std::invalid_argument("conv3_pool_win_x6: frame shape out of range");
-    const int tiles = N * ((H + V_TH - 1) / V_TH) * ((W + V_TW - 1) / V_TW);
-    if (f32_in)
-        hipLaunchKernelGGL(conv3_pool_win_x6_kernel<true>, dim3(tiles), dim3(64 * V_NW), 0, st, in, ips, N, H, W, wt,
-                           bias, out, ops);
-    else
-        hipLaunchKernelGGL(conv3_pool_win_x6_kernel<false>, dim3(tiles), dim3(64 * V_NW), 0, st, in, ips, N, H, W, wt,
-                           bias, out, ops);
+    Conv1Segs S{};
+    S.n = 1;
+    S.s[0] = Conv1Seg{in, out, ips, ops, N, H, W, 0};
+    launch_conv3_pool_win_x6_segs(S, wt, bias, f32_in, st);
 }
 
 void launch_maxpool_x6(const uint8_t* in, uint32_t ips, uint8_t* out, uint32_t ops, int NG, int H, int W,

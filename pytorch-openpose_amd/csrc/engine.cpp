@@ -1455,14 +1455,39 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
             DevConv* c2 = find_conv(h, net, vgg[1].name);
             const bool pair12 = conv12_win_ok(vgg[1], c2);
             const bool f32 = pair12 && h->c11_f32;
-            if (ns > 1 && ns <= (size_t)kMaxScales && h->scale_streams && pair12) {
-                // a pyramid's conv1_1 -> conv1_2 chains (their own kernels, one launch per
-                // segment) on concurrent streams: the small scales' launches fill the large
-                // scale's tail instead of running one after another
-                run_scales_concurrently(h, (int)ns, [&](int i) {
-                    conv11_direct((size_t)i, s, c, f32);
-                    conv12_win((size_t)i, vgg[1], c2, 0);
-                });
+            if (ns > 1 && ns <= (size_t)kConv1Segs && pair12) {
+                // a pyramid's conv1_1 and conv1_2 as one launch each over every segment: the
+                // small scales' tiles fill the large scale's tail (round 3 ran the per-scale
+                // chains on concurrent streams, which a captured graph may not fork any more)
+                Conv1Segs S1{}, S2{};
+                S1.n = S2.n = (int)ns;
+                double f1 = 0, f2 = 0;
+                long px1 = 0, px2 = 0;
+                for (size_t i = 0; i < ns; ++i) {
+                    const NetSeg& sg = segs[i];
+                    const size_t npix = (size_t)sg.N * sg.Hp * sg.Wp;
+                    const size_t npo = (size_t)sg.N * (sg.Hp / 2) * (sg.Wp / 2);
+                    bs[i].cur = x6act(bs[i].A, 8, 0, sg.N, sg.Hp, sg.Wp);  // conv1_1's output
+                    const XAct o2 = out_buf(i, 1, 8);                        // (not A)
+                    if (o2.p == bs[i].A) throw std::logic_error("conv1_2 output aliases its input");
+                    S1.s[i] = Conv1Seg{sg.x, bs[i].A, 0u, (uint32_t)(npix * 8 * 16), sg.N, sg.Hp, sg.Wp, 0};
+                    S2.s[i] = Conv1Seg{bs[i].A, static_cast<uint8_t*>(o2.p), (uint32_t)(npix * 8 * 16),
+                                       (uint32_t)(npo * 8 * 16), sg.N, sg.Hp, sg.Wp, 0};
+                    f1 += 2.0 * 64 * 27 * (double)npix;
+                    f2 += 2.0 * 64 * 576 * (double)(npo * 4);
+                    px1 += (long)npix;
+                    px2 += (long)npo * 4;
+                    bs[i].cur = o2;
+                }
+                ProfEntry pe;
+                h->prof_begin(pe, "conv3x3", f1, 0);
+                if (h->detail) pe.detail = "layer/" + s.name + "/first_direct/g" + std::to_string(ns) + "/n" + std::to_string(px1);
+                launch_conv_first_x6_segs(S1, c->wt, c->Mpad, c->bias, f32, h->stream);
+                h->prof_end(pe);
+                h->prof_begin(pe, "conv3x3", f2, 0);
+                if (h->detail) pe.detail = "layer/" + vgg[1].name + "/x6win/g" + std::to_string(ns) + "/n" + std::to_string(px2);
+                launch_conv3_pool_win_x6_segs(S2, c2->wx6, c2->bias, f32, h->stream);
+                h->prof_end(pe);
                 ++li;
                 ++lvl;
                 continue;

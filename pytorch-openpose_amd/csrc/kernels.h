@@ -46,6 +46,22 @@ void launch_to_x6(const float* in, int cstride, int coff, int C, int N, int HW, 
 void launch_from_x6(const uint8_t* in, int cg, int goff, uint32_t ps, int C, int N, int HW, float* out, int cstride,
                     int coff, hipStream_t st);
 // f32_out: fp32 units of 8 channels ([N][8][H*W] x 32 bytes) for launch_conv3_pool_win_x6's f32_in
+// conv1_1 / conv1_2 of a pyramid's scales in one launch each: one segment per scale (input,
+// output, piece strides, geometry); b0 is set by the launcher
+constexpr int kConv1Segs = 8;
+struct Conv1Seg {
+    const void* in;
+    uint8_t* out;
+    uint32_t ips, ops;
+    int N, H, W, b0;
+};
+struct Conv1Segs {
+    Conv1Seg s[kConv1Segs];
+    int n;
+};
+void launch_conv_first_x6_segs(Conv1Segs segs, const float* wt, int Mpad, const float* bias, bool f32_out,
+                               hipStream_t st);
+void launch_conv3_pool_win_x6_segs(Conv1Segs segs, const uint8_t* wt, const float* bias, bool f32_in, hipStream_t st);
 void launch_conv_first_x6(const float* x, int N, int Cin, int H, int W, const float* wt, int Mpad, const float* bias,
                           uint8_t* out, uint32_t ops, bool f32_out, hipStream_t st);
 // zero the padding units of `planes` X6P (piece, group) planes of an N x H x W buffer (common.h)
