@@ -97,25 +97,30 @@ def test_pipelined_multiscale_matches_serial():
 
 
 def test_hand_scale_streams_bit_identical():
-    """Hand(): the per-scale work that runs on concurrent streams by default (the lockstep
-    pyramid's conv1_1 -> conv1_2 chains, one stream per scale) and the same work one launch
-    after another (OPOSE_SCALE_STREAMS=0, read when the handle is created) give identical peaks."""
+    """Hand() with one network per scale (OPOSE_LOCKSTEP=0): the scales' networks on concurrent
+    streams (default) and one after another (OPOSE_SCALE_STREAMS=0, read when the handle is
+    created) give identical peaks -- and equal the default lockstep pyramid's."""
     from src.hand import Hand
     from src.weights import seeded_state_dict
     crop = np.random.default_rng(14).integers(0, 256, (150, 150, 3), dtype=np.uint8)
     sd = seeded_state_dict("hand", 0)
-    a = Hand(sd)(crop)
-    old = os.environ.get("OPOSE_SCALE_STREAMS")
-    os.environ["OPOSE_SCALE_STREAMS"] = "0"
-    try:
-        serial = Hand(sd)
-    finally:
-        if old is None:
-            del os.environ["OPOSE_SCALE_STREAMS"]
-        else:
-            os.environ["OPOSE_SCALE_STREAMS"] = old
-    b = serial(crop)
-    assert a.dtype == b.dtype and np.array_equal(a, b)
+
+    def make(env):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            return Hand(sd)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    concurrent = make({"OPOSE_LOCKSTEP": "0"})(crop)
+    serial = make({"OPOSE_LOCKSTEP": "0", "OPOSE_SCALE_STREAMS": "0"})(crop)
+    lockstep = Hand(sd)(crop)
+    for b in (serial, lockstep):
+        assert concurrent.dtype == b.dtype and np.array_equal(concurrent, b)
 
 
 def test_graph_replay_equals_eager():
