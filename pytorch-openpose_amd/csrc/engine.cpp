@@ -99,6 +99,14 @@ std::vector<Spec> state_dict_order(int net) {
 
 int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
+// OPOSE_PIPELINE_DEFER gate: the layer before which the next network records it ("stageN": before
+// CPM stage N).  Swept on the bench, same box: conv4_1 2,101, stage2 2,100, stage3 2,105, stage4
+// 2,107 frames/s against 2,110 with no gate (scripts/r4_gate_ab.sh, then with an env override)
+static const std::string& gate_layer() {
+    static const std::string g = "conv3_1";
+    return g;
+}
+
 // ---------------------------------------------------------------- streams
 // Streams come from a process-wide pool and go back to it when a handle is destroyed (drained
 // first), so test suites and services that create and destroy handles do not churn HIP streams.
@@ -1447,7 +1455,7 @@ static void run_trunk_x6(opose_ctx* h, int net, const std::vector<NetSeg>& segs,
     for (size_t li = 0; li < vgg.size(); ++li) {
         const Spec& s = vgg[li];
         DevConv* c = find_conv(h, net, s.name);
-        if (h->gate_ev && s.name == "conv3_1") {  // OPOSE_PIPELINE_DEFER: the previous post may start
+        if (h->gate_ev && s.name == gate_layer()) {  // OPOSE_PIPELINE_DEFER: the previous post may start
             OPOSE_HIP_CHECK(hipEventRecord(h->gate_ev, h->stream));
             h->gate_done = true;
         }
@@ -1723,6 +1731,10 @@ static std::vector<float*> body_net_x6(opose_ctx* h, const std::vector<NetSeg>& 
     int cur = 1;
     for (int st = 2; st <= 6; ++st) {
         const std::string sf = "_stage" + std::to_string(st);
+        if (h->gate_ev && gate_layer() == "stage" + std::to_string(st)) {
+            OPOSE_HIP_CHECK(hipEventRecord(h->gate_ev, h->stream));
+            h->gate_done = true;
+        }
         layer("Mconv1" + sf + "_L1+L2", "", [&](size_t i) { return s_(i, cur, 0); },
               [&](size_t i) { return t_(i, 0, 0); }, none, none, true, false);
         int t = 0;
