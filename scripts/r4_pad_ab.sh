@@ -1,5 +1,5 @@
-# same-box A/B of the X6P row pad (alt_lib/pad3.so: 3 zero units, default: 16)
-# alt_lib/pad3.so: scripts/build_alt.sh HEAD pad3 after setting kX6PPad = 16 -> 3 (or the reverse) in the worktree
+# Same-box A/B of the X6P row pad, measured while the tree had kX6PPad = 16: alt_lib/pad3.so was
+# that tree built with 3 (scripts/build_alt.sh on a worktree edited to 3).  The tree now has 3.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export PYTHONDONTWRITEBYTECODE=1
 for r in 1 2; do for v in pad3 pad16; do
   if [ $v = pad3 ]; then export OPOSE_LIB=alt_lib/pad3.so; else unset OPOSE_LIB; fi
