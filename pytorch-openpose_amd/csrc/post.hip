@@ -908,50 +908,78 @@ __global__ __launch_bounds__(256) void limb_greedy(const double* __restrict__ sc
     if (tid == 0) conn_cnt[nk] = count;
 }
 
-// One wavefront per frame: sequential person assembly with lane-parallel row scans.
+// One wavefront per frame: sequential person assembly with lane-parallel row scans.  Every
+// limb's connections (score, both candidates' scores, candidate indices) are staged into LDS in
+// one parallel pass when they fit `stage` entries (the serial loop then reads LDS only, and the
+// dependent global loads -- count, connection, candidate score -- are paid once per frame instead
+// of once per limb); otherwise limb by limb.
 __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ conn, const int* __restrict__ conn_cnt,
                                                       const int* __restrict__ part_cnt, RecordLayout L,
-                                                      uint8_t* __restrict__ records) {
-    // [max_people][20] subset rows, then the current limb's connections staged from global memory
-    // (score, both candidates' scores, candidate indices): the serial loop below reads LDS only
+                                                      uint8_t* __restrict__ records, int stage) {
+    // [max_people][20] subset rows, then the staged connections
     extern __shared__ double smem[];
     const int n = blockIdx.x;
     const int lane = threadIdx.x;
     const int cap = L.peaks_per_part, maxp = L.max_people;
     double* s_sub = smem;
     double* s_cs = smem + (size_t)maxp * 20;
-    double* s_sa = s_cs + cap;
-    double* s_sb = s_sa + cap;
-    int* s_ci = reinterpret_cast<int*>(s_sb + cap);
+    double* s_sa = s_cs + stage;
+    double* s_sb = s_sa + stage;
+    int* s_ci = reinterpret_cast<int*>(s_sb + stage);
     uint8_t* rec = records + (size_t)n * L.bytes;
     int32_t* hdr = reinterpret_cast<int32_t*>(rec);
     const double* cand = reinterpret_cast<const double*>(rec + L.cand_off);
     double* outsub = reinterpret_cast<double*>(rec + L.subset_off);
-    __shared__ int s_start[18];
+    __shared__ int s_start[18], s_nc[19], s_off[20];
     if (lane < 18) {
         int acc = 0;
         for (int p = 0; p < lane; ++p) acc += part_cnt[n * 18 + p];
         s_start[lane] = acc;
     }
+    if (lane < 19) s_nc[lane] = conn_cnt[n * 19 + lane];
     __syncthreads();
+    if (lane == 0) {
+        int acc = 0;
+        for (int k = 0; k < 19; ++k) {
+            s_off[k] = acc;
+            acc += max(s_nc[k], 0);
+        }
+        s_off[19] = acc;
+    }
+    __syncthreads();
+    // stage connection c of limb k at entry e
+    auto stage_one = [&](int k, int c, int e) __attribute__((always_inline)) {
+        const Conn cc = conn[((size_t)n * 19 + k) * cap + c];
+        const int ga = s_start[kLimbA[k]] + cc.i, gb = s_start[kLimbB[k]] + cc.j;
+        s_cs[e] = cc.s;
+        s_sa[e] = cand[(size_t)ga * 4 + 2];
+        s_sb[e] = cand[(size_t)gb * 4 + 2];
+        s_ci[2 * e] = ga;
+        s_ci[2 * e + 1] = gb;
+    };
+    const bool all = s_off[19] <= stage;
+    if (all) {
+        for (int e = lane; e < s_off[19]; e += 64) {
+            int k = 0;
+            while (k < 18 && e >= s_off[k + 1]) ++k;
+            stage_one(k, e - s_off[k], e);
+        }
+        __syncthreads();
+    }
     int status = hdr[0];
     int nrows = 0;
     for (int k = 0; k < 19 && status == 0; ++k) {
-        const int nc = conn_cnt[n * 19 + k];
+        const int nc = s_nc[k];
         if (nc < 0) continue;
         const int ia = kLimbA[k], ib = kLimbB[k];
-        const Conn* ck = conn + ((size_t)n * 19 + k) * cap;
-        for (int c = lane; c < nc; c += 64) {
-            const Conn cc = ck[c];
-            const int ga = s_start[ia] + cc.i, gb = s_start[ib] + cc.j;
-            s_cs[c] = cc.s;
-            s_sa[c] = cand[(size_t)ga * 4 + 2];
-            s_sb[c] = cand[(size_t)gb * 4 + 2];
-            s_ci[2 * c] = ga;
-            s_ci[2 * c + 1] = gb;
+        int base = s_off[k];
+        if (!all) {
+            base = 0;
+            for (int c = lane; c < nc; c += 64) stage_one(k, c, c);
+            __syncthreads();
         }
-        __syncthreads();
-        for (int c = 0; c < nc; ++c) {
+        for (int c0 = 0; c0 < nc; ++c0) {
+            const int c = base + c0;
             const double idA = (double)s_ci[2 * c];
             const double idB = (double)s_ci[2 * c + 1];
             const double s = s_cs[c];
@@ -1015,7 +1043,7 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
             }
             __syncthreads();
         }
-        __syncthreads();  // the staged connections are re-filled by the next limb
+        if (!all) __syncthreads();  // the staged connections are re-filled by the next limb
     }
     // prune (src/body.py:203-208) and emit in order
     int kept = 0;
@@ -1086,7 +1114,13 @@ void launch_limb_greedy(const double* score, const int* part_cnt, int N, int cap
 
 void launch_assemble(const Conn* conn, const int* conn_cnt, const int* part_cnt, int N, const RecordLayout& L,
                      uint8_t* records, hipStream_t st) {
-    const size_t shm = sizeof(double) * 20 * L.max_people + (size_t)L.peaks_per_part * (3 * sizeof(double) + 2 * sizeof(int));
+    // staged connection entries: every limb's (19 x peaks_per_part) when that fits 64 KB with the
+    // subset rows, at least one limb's
+    constexpr size_t kEntry = 3 * sizeof(double) + 2 * sizeof(int);
+    const size_t sub = sizeof(double) * 20 * L.max_people;
+    const size_t fit = sub < 64 * 1024 ? (64 * 1024 - sub) / kEntry : 0;
+    const int stage = (int)std::max<size_t>((size_t)L.peaks_per_part, std::min<size_t>(19 * (size_t)L.peaks_per_part, fit));
+    const size_t shm = sub + (size_t)stage * kEntry;
     if (shm > 64 * 1024) {  // grown capacities (up to 256 people / 1024 peaks per part: 80 KB)
         static size_t granted = 0;
         if (shm > granted) {
@@ -1095,7 +1129,7 @@ void launch_assemble(const Conn* conn, const int* conn_cnt, const int* part_cnt,
             granted = shm;
         }
     }
-    hipLaunchKernelGGL(assemble_people, dim3(N), dim3(64), shm, st, conn, conn_cnt, part_cnt, L, records);
+    hipLaunchKernelGGL(assemble_people, dim3(N), dim3(64), shm, st, conn, conn_cnt, part_cnt, L, records, stage);
 }
 
 }  // namespace opose
