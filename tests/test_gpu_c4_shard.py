@@ -3,15 +3,15 @@
 bench.py (main, `step`) runs, per GPU: `Body(seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE))`,
 32 uniform-random 368x656 uint8 frames (rng seed 1 + rank) resident in HBM, and
 `Body.infer_records(frames, rec, pipeline=True)` every step.  At batch 32 the conv planner picks
-the data-parallel 128x256 grids, not the stream-K grids of the small batches the other tests use,
+the data-parallel 128x256 grids (one k slab per tile), not the multi-slab grids of the small batches the other tests use,
 so this module pins the very launch sequence behind the bench's `value`:
 
 (a) all 32 decoded records, serial and pipelined (several back-to-back pipelined steps, the
     bench's own overlap), equal the oracle's post-network restatement (src/body.py:52-212) on the
     GPU network's maps of the same batch, bit for bit;
-(b) two of the 32 frames end to end against the oracle network + post (the north-star bar of
-    test_gpu_parity.test_body_end_to_end_vs_reference: identical keypoint pixels, ids and
-    person/subset assignment, scores within 1e-3);
+(b) two of the 32 frames end to end against the float64 oracle network + post: every keypoint at
+    a float64 keypoint's pixel or tipped across a float64 plateau, none elsewhere, people within
+    one (these crowded frames have plateaus that any fp32 evaluation tips);
 (c) one frame's batch-32 network maps against oracle.network.body_forward within the network
     tolerance (the exact 128x256 grids the bench runs).
 
@@ -80,69 +80,82 @@ def test_c4_shard_records_exact_vs_oracle(body, gpu_maps, records, lo):
             assert np.array_equal(s, ref_s), f"frame {f}: subsets differ"
 
 
-def _peak_agreement(c1, c2):
-    """Match keypoints (x, y, score, id rows) of two candidate arrays: the same position first,
-    else within 1 px (Chebyshev); a match also needs the score (the part's heat value at the
-    peak) within 1e-3 relative, which keeps peaks of different parts apart -> (exact,
-    within_1px, unmatched)."""
-    free = [tuple(r[:3]) for r in c2]
-    exact = near = 0
+def _keypoints_vs_f64(img, cand, sd64, thre1=0.1, tol=1e-5):
+    """Every keypoint of `cand` against the float64 network's (the exact answer): at a float64
+    keypoint's pixel, or one pixel from a float64 keypoint of the same part where the float64
+    smoothed heat map (the map the peak search runs on, src/body.py:76-80) takes values within
+    `tol` of its maximum at both pixels (a plateau the fp32 summation order may tip), or, for a
+    keypoint on one side only, where that smoothed value is within `tol` of thre1.  Returns
+    (exact, tied, bad, n_f64, people_f64)."""
+    from scipy.ndimage import gaussian_filter
+    from oracle import body_post, network
+    H, W = img.shape[:2]
+    x, pad, phw = body_post.preprocess(img, 0.5)
+    cap = {}
+
+    def fn(xx):
+        p, h = network.body_forward(torch.from_numpy(xx).double(), sd64)
+        cap["h"] = h.float().numpy()
+        return p.float().numpy(), cap["h"]
+    c64, s64 = body_post.body_infer(img, fn)
+    c64 = np.asarray(c64)
+    up = body_post.upsample_map(cap["h"][0], pad, phw, (H, W))  # [H, W, 19]
+    blur = [gaussian_filter(up[:, :, p].astype(np.float64), sigma=3) for p in range(18)]
+    top = [b.max() for b in blur]
+
+    def part(r):  # the part whose map holds the keypoint's score (its raw heat value) there
+        return int(np.argmin(np.abs(up[int(r[1]), int(r[0]), :18] - r[2])))
+    p64 = [part(r) for r in c64]
+    free = set(range(len(c64)))
+    exact = tied = bad = 0
     rest = []
-
-    def close(p, q, tol):
-        return abs(q[0] - p[0]) <= tol and abs(q[1] - p[1]) <= tol and abs(q[2] - p[2]) <= 1e-3 * abs(q[2]) + 1e-6
-
-    for r in c1:
-        p = tuple(r[:3])
-        hit = next((q for q in free if close(p, q, 0)), None)
-        if hit is None:
-            rest.append(p)
+    for r in cand:
+        j = next((j for j in free if c64[j, 0] == r[0] and c64[j, 1] == r[1] and p64[j] == part(r)), None)
+        if j is None:
+            rest.append(r)
         else:
-            free.remove(hit)
+            free.discard(j)
             exact += 1
-    unmatched = 0
-    for p in rest:
-        hit = next((q for q in free if close(p, q, 1)), None)
-        if hit is None:
-            unmatched += 1
+    for r in rest:
+        p, xg, yg = part(r), int(r[0]), int(r[1])
+        j = next((j for j in free if p64[j] == p and abs(c64[j, 0] - xg) <= 1 and abs(c64[j, 1] - yg) <= 1 and
+                  abs(blur[p][yg, xg] - blur[p][int(c64[j, 1]), int(c64[j, 0])]) <= tol * top[p]), None)
+        if j is not None:
+            free.discard(j)
+            tied += 1
+        elif abs(blur[p][yg, xg] - thre1) <= tol * top[p]:
+            tied += 1
         else:
-            free.remove(hit)
-            near += 1
-    return exact, near, unmatched + len(free)
+            bad += 1
+    for j in free:  # float64 keypoints with no counterpart: threshold ties only
+        p = p64[j]
+        if abs(blur[p][int(c64[j, 1]), int(c64[j, 0])] - thre1) <= tol * top[p]:
+            tied += 1
+        else:
+            bad += 1
+    return exact, tied, bad, len(c64), len(s64)
 
 
 @pytest.mark.parametrize("f", [0, 31])
 def test_c4_shard_end_to_end_vs_oracle(records, frames_np, f):
     """End to end against the oracle network + post.  On these calibrated crowded frames (~300
-    keypoints, ~20 people) the smoothed heat maps have 1-2 px plateaus: any two fp32 evaluations
-    of the network put some peaks one pixel apart -- the reference's own torch-CPU network on 8
-    threads and on 1 thread disagree on 12.4 % of the keypoint positions on average.  So the bar is
-    set against the float64 network (the exact answer) and relative to the reference's own fp32:
-    at most 2 keypoints more than the torch-fp32 network without a float64 keypoint within 1 px
-    (a smoothed value within fp32 noise of thre1 may appear or vanish: < 1 % of ~300), no more
-    1-px shifts than 1.5x the torch-fp32 network's, and the same number of people within one."""
-    from oracle import body_post, network
+    keypoints, ~20 people) the smoothed heat maps have 1-px plateaus whose two pixels differ by
+    < 1e-8 of the map in the float64 network: any fp32 evaluation tips some of them (torch-CPU
+    fp32 moves 39 of 303 keypoints on frame 0, 37 of 302 on frame 31, every one onto a plateau;
+    its 8- vs 1-thread runs disagree on 12.4 % on average, scripts/fp32_thread_noise.py).  The bar
+    is the float64 network's keypoints: each GPU keypoint at a float64 keypoint's pixel or tipped
+    across a plateau (smoothed values within 1e-5 of the map, _keypoints_vs_f64), none elsewhere,
+    and the people count within one of the float64 answer (a tipped keypoint changes limb scores,
+    and torch-fp32 itself differs by one person on frame 31)."""
+    from oracle import network
     from src.weights import BENCH_OUT_SCALE
-    sd = network.seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE)
-    sd64 = {k: v.double() for k, v in sd.items()}
-
-    def net_fn(d, dbl):
-        def fn(x):
-            xx = torch.from_numpy(x)
-            p, h = network.body_forward(xx.double() if dbl else xx, d)
-            return p.float().numpy(), h.float().numpy()
-        return fn
-
-    ref64_c, ref64_s = body_post.body_infer(frames_np[f], net_fn(sd64, True))
-    ref32_c, _ = body_post.body_infer(frames_np[f], net_fn(sd, False))
+    sd64 = {k: v.double() for k, v in network.seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE).items()}
     cand, subset = records[0][f]
-    e_gpu, n_gpu, u_gpu = _peak_agreement(cand, ref64_c)
-    e_ref, n_ref, u_ref = _peak_agreement(ref32_c, ref64_c)
-    print(f"frame {f}: gpu vs f64 exact {e_gpu} 1px {n_gpu} unmatched {u_gpu}; "
-          f"torch-fp32 vs f64 exact {e_ref} 1px {n_ref} unmatched {u_ref}; people {len(subset)} vs {len(ref64_s)}")
-    assert u_gpu <= u_ref + 2
-    assert n_gpu <= 1.5 * n_ref + 5
-    assert abs(len(subset) - len(ref64_s)) <= 1
+    exact, tied, bad, n64, people64 = _keypoints_vs_f64(frames_np[f], cand, sd64)
+    print(f"frame {f}: {len(cand)} GPU keypoints vs {n64} float64: {exact} exact, {tied} on plateaus, {bad} off; "
+          f"people {len(subset)} vs {people64}")
+    assert bad == 0 and len(cand) <= n64 + tied
+    assert abs(len(subset) - people64) <= 1
 
 
 def test_c4_shard_network_maps_vs_oracle(gpu_maps, frames_np):
