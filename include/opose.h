@@ -45,6 +45,8 @@ typedef enum opose_status {
     OPOSE_E_CAPACITY = -5,   /* a per-frame record overflowed (peaks/people)        */
     OPOSE_E_ASSEMBLY = -6,   /* reference IndexError: a 3rd subset row matched a
                                 connection (src/body.py:170-173)                    */
+    OPOSE_E_TIMEOUT = -7,    /* opose_rccl_wait: the halo exchange made no progress
+                                before the deadline (communicator aborted)          */
 } opose_status;
 
 enum { OPOSE_NET_BODY = 0, OPOSE_NET_HAND = 1 };
@@ -190,9 +192,19 @@ typedef int (*opose_halo_fn)(void* user, size_t bytes, void* stream);
  * between the stage layers). */
 int opose_rccl_unique_id(void* id, size_t len);  /* len >= 128; call on one rank, share the bytes */
 int opose_rccl_init(opose_t* h, const void* id, int rank, int nranks);
-/* A band rank failed: ncclCommAbort on the handle's communicator (the peers' pending halo
- * send / recv fail instead of waiting) and drop it; opose_rccl_init builds a new one. */
+/* A band rank failed: ncclCommAbort on the handle's communicator (this rank's own queued halo
+ * send / recv exit) and drop it; opose_rccl_init builds a new one.  The abort does not reach the
+ * neighbours' queued kernels: they bound their wait with opose_rccl_wait. */
 int opose_rccl_abort(opose_t* h);
+/* Wait for the handle's stream (where the RCCL halo send / recv of opose_body_band_maps run) with a
+ * deadline.  Returns OPOSE_OK when the work completed.  If the communicator reports an
+ * asynchronous error, or the stream is still busy after timeout_ms (a band neighbour failed and
+ * will never post its side of an exchange), the handle's own communicator is aborted: RCCL's abort
+ * flag makes this rank's queued send / recv kernels exit, so the stream drains instead of waiting
+ * forever; returns OPOSE_E_HIP / OPOSE_E_TIMEOUT, and opose_rccl_init builds a new communicator.
+ * A failing rank's ncclCommAbort cannot reach its neighbours' queued kernels (xGMI P2P has no
+ * peer-failure signal), so each neighbour bounds its own wait with this call (src/dist.py). */
+int opose_rccl_wait(opose_t* h, int timeout_ms);
 int opose_set_band_peers(opose_t* h, int up, int dn);  /* communicator ranks; -1: none */
 size_t opose_body_band_halo_bytes(int wl);
 int opose_body_band_maps(opose_t* h, const uint8_t* bgr, int H, int W, int64_t row_stride,

@@ -25,6 +25,7 @@
 #include <mutex>
 #include <memory>
 #include <string>
+#include <thread>
 #include <queue>
 #include <vector>
 
@@ -624,6 +625,7 @@ struct Rccl {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommGetAsyncError) async_error = nullptr;
 };
 static const Rccl& rccl() {
     static const Rccl r = [] {
@@ -646,6 +648,7 @@ static const Rccl& rccl() {
         x.group_start = reinterpret_cast<decltype(x.group_start)>(sym("ncclGroupStart"));
         x.group_end = reinterpret_cast<decltype(x.group_end)>(sym("ncclGroupEnd"));
         x.error_string = reinterpret_cast<decltype(x.error_string)>(sym("ncclGetErrorString"));
+        x.async_error = reinterpret_cast<decltype(x.async_error)>(sym("ncclCommGetAsyncError"));
         return x;
     }();
     return r;
@@ -2159,11 +2162,22 @@ static void batch_post_common(opose_ctx* h, int N, int H, int W, const float* ma
 
 // Run `work` (device work only: kernels, device memsets/copies on h->stream, no host sync,
 // no allocation once warm) through the launch-sequence cache keyed by `key`.  Captures stay on
-// the one stream (h->capturing: run_scales_concurrently runs its scales one after another): on
-// this stack, destroying executable graphs whose capture forked onto other streams made later
-// graph launches of other handles segfault inside hipGraphLaunch -- 2 of 2 runs of the GPU test
-// list, 0 of 2 with the forks kept out of captures or with no executable graph destroyed
-// (round 4; the eager first call of a signature still runs the scales concurrently).
+// the one stream (h->capturing: run_scales_concurrently runs its scales one after another), and
+// a captured graph that is not a single chain of nodes is refused (linear_graph).  Cause: in a
+// torch process the library runs on torch's bundled HIP runtime (libamdhip64 7.0.2, SONAME
+// libamdhip64.so.7, loaded before ours), whose hipGraphLaunch segfaults on a freshly instantiated
+// forked graph after other forked executables were destroyed.  scripts/graph_fork_repro.hip
+// reproduces it without libopose: the same program crashes under 7.0.2 and runs clean
+// under /opt/rocm's 7.2, with no fork in captures, or with no executable destroyed.
+// one root and every other node entered by exactly one edge from a chain: nodes - 1 edges
+static bool linear_graph(hipGraph_t g) {
+    size_t nodes = 0, edges = 0, roots = 0;
+    OPOSE_HIP_CHECK(hipGraphGetNodes(g, nullptr, &nodes));
+    OPOSE_HIP_CHECK(hipGraphGetEdges(g, nullptr, nullptr, &edges));
+    OPOSE_HIP_CHECK(hipGraphGetRootNodes(g, nullptr, &roots));
+    return nodes == 0 || (roots == 1 && edges == nodes - 1);
+}
+
 template <class F>
 static void run_graphed(opose_ctx* h, const std::string& key, F&& work) {
     if (!h->use_graphs || h->prof || !h->stream) {
@@ -2197,6 +2211,11 @@ static void run_graphed(opose_ctx* h, const std::string& key, F&& work) {
     }
     hipGraph_t g = nullptr;
     OPOSE_HIP_CHECK(hipStreamEndCapture(h->stream, &g));
+    if (!linear_graph(g)) {  // a fork inside a capture: never instantiated (see above)
+        (void)hipGraphDestroy(g);
+        throw std::logic_error("libopose: a captured launch sequence forked onto another stream (" + key.substr(0, key.find('|')) +
+                               "); captures must stay on one stream (HIP 7.0.2 hipGraphLaunch bug, DESIGN §5)");
+    }
     if (g_alloc_epoch.load() != epoch) {  // something allocated inside the capture: not replayable
         (void)hipGraphDestroy(g);
         h->graphs.erase(key);
@@ -2833,6 +2852,37 @@ int opose_rccl_abort(opose_t* h) {
             rccl_check(rccl().comm_abort(c));
         }
         return OPOSE_OK;
+    });
+}
+
+int opose_rccl_wait(opose_t* h, int timeout_ms) {
+    if (!h || timeout_ms < 0) return OPOSE_E_ARG;
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t q = hipStreamQuery(h->stream);
+            if (q == hipSuccess) return OPOSE_OK;
+            if (q != hipErrorNotReady) OPOSE_HIP_CHECK(q);
+            ncclResult_t ae = ncclSuccess;
+            if (h->comm) rccl_check(rccl().async_error(h->comm, &ae));
+            const bool late = std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms);
+            if ((ae != ncclSuccess && ae != ncclInProgress) || late) {
+                // a band neighbour failed or never arrived: abort this rank's communicator, which
+                // raises RCCL's abort flag that the queued send / recv kernels poll, so this rank's
+                // stream drains instead of waiting on a peer that will not come
+                if (h->comm) {
+                    ncclComm_t c = h->comm;
+                    h->comm = nullptr;
+                    h->band_up = h->band_dn = -1;
+                    (void)rccl().comm_abort(c);
+                }
+                h->err = late ? "RCCL halo exchange: no progress within the deadline (communicator aborted)"
+                              : std::string("RCCL halo exchange: ") + rccl().error_string(ae) + " (communicator aborted)";
+                return late ? OPOSE_E_TIMEOUT : OPOSE_E_HIP;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
     });
 }
 

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("OPOSE_LIB", os.path.join(os.path.dirname(_HERE), "lib
 
 OPOSE_OK = 0
 OPOSE_E_ARG, OPOSE_E_SHAPE, OPOSE_E_HIP, OPOSE_E_WEIGHTS, OPOSE_E_CAPACITY, OPOSE_E_ASSEMBLY = -1, -2, -3, -4, -5, -6
+OPOSE_E_TIMEOUT = -7
 NET_BODY, NET_HAND = 0, 1
 IN_DEVICE, OUT_DEVICE, PIPELINE, PIPELINE_DEFER = 1, 2, 4, 8
 MAX_SCALES = 8
@@ -62,6 +63,7 @@ def _load():
         "opose_rccl_unique_id": (I, [P, S]),
         "opose_rccl_init": (I, [P, P, I, I]),
         "opose_rccl_abort": (I, [P]),
+        "opose_rccl_wait": (I, [P, I]),
         "opose_set_band_peers": (I, [P, I, I]),
         "opose_body_band_maps": (I, [P, P, I, I, C.c_int64, C.POINTER(Params), I, I, I, P, HALO_FN, P, P, S, I]),
         "opose_hand_infer": (I, [P, P, I, I, I, C.c_int64, C.c_int64, C.POINTER(Params), P, P, I]),
@@ -100,7 +102,7 @@ EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last
             "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_hand_forward_pyramid",
             "opose_body_infer",
             "opose_body_post", "opose_body_scale_geom", "opose_body_scale_maps",
-            "opose_body_post_scales", "opose_body_band_halo_bytes", "opose_body_band_maps", "opose_rccl_unique_id", "opose_rccl_init", "opose_rccl_abort", "opose_set_band_peers", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
+            "opose_body_post_scales", "opose_body_band_halo_bytes", "opose_body_band_maps", "opose_rccl_unique_id", "opose_rccl_init", "opose_rccl_abort", "opose_rccl_wait", "opose_set_band_peers", "opose_batch_body_infer", "opose_batch_body_post", "opose_batch_hand_infer", "opose_batch_hand_post", "opose_hand_infer", "opose_hand_infer_crops", "opose_hand_post", "opose_profile_enable",
             "opose_profile_reset", "opose_profile_read", "opose_debug_conv", "opose_debug_conv_time", "opose_debug_conv_x6", "opose_debug_conv_x6_time", "opose_debug_preprocess",
             "opose_debug_heat", "opose_debug_hand_label"]
 
@@ -211,8 +213,18 @@ class Handle:
         self.check(lib.opose_rccl_init(self.h, buf, int(rank), int(nranks)))
 
     def rccl_abort(self):
-        """ncclCommAbort on the band communicator (a failed band rank's neighbours stop waiting)."""
+        """ncclCommAbort on the band communicator: this rank's own queued halo send / recv exit.
+        It does not reach the neighbours' queued kernels; they bound their wait with rccl_wait."""
         self.check(lib.opose_rccl_abort(self.h))
+
+    def rccl_wait(self, timeout_s: float):
+        """Wait for the handle's stream (the RCCL halo exchanges of band_maps) for at most
+        timeout_s.  A neighbour that failed, or an asynchronous RCCL error, makes the library abort
+        this rank's communicator so its queued send / recv exit: TimeoutError / OposeError."""
+        rc = lib.opose_rccl_wait(self.h, max(0, int(timeout_s * 1000)))
+        if rc == OPOSE_E_TIMEOUT:
+            raise TimeoutError((lib.opose_last_error(self.h) or b"").decode())
+        self.check(rc)
 
     def set_band_peers(self, up, dn):
         self.check(lib.opose_set_band_peers(self.h, -1 if up is None else int(up), -1 if dn is None else int(dn)))

@@ -188,23 +188,29 @@ def band_exchange(rank_up, rank_dn, group=None):
     return ex
 
 
-def abort_band_group(body, group=None, rccl: bool = False):
+def abort_band_group(body, group=None, rccl: bool = False, destroy_group: bool = False):
     """A band rank failed mid-frame: its neighbours are (or will be) blocked in one of the 27
-    halo exchanges.  Abort what they wait on -- the library's RCCL communicator (ncclCommAbort:
-    their pending send / recv fail) and the torch process group (gloo: the peers' pending
-    send / recv see the closed connections) -- so they raise instead of hanging until the
-    backend timeout.  The process group is unusable afterwards."""
+    halo exchanges.
+    RCCL: abort the library's communicator on this rank (its own queued send / recv exit).  The
+    abort cannot reach the neighbours' queued kernels (xGMI P2P has no peer-failure signal); each
+    neighbour bounds its own wait with Handle.rccl_wait (body_scale_sharded's band_timeout) and
+    aborts its communicator when the deadline passes.  The torch process group is left alone.
+    gloo: the exchange runs through the torch process group, so only destroying it releases the
+    peers' pending send / recv.  That happens only when the caller opts in (destroy_group), and then
+    to `group` -- the default (WORLD) group when group is None."""
     if rccl:
         try:
             body.handle.rccl_abort()
         except Exception:
             pass
         body._band_comm = None
-    try:
-        if dist.is_initialized():
-            dist.destroy_process_group(group)
-    except Exception:
-        pass
+        return
+    if destroy_group:
+        try:
+            if dist.is_initialized():
+                dist.destroy_process_group(group)
+        except Exception:
+            pass
 
 
 def init_band_comm(body, group=None):
@@ -224,7 +230,7 @@ def init_band_comm(body, group=None):
 
 
 def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=None, split: str = "balanced",
-                       maps_out=None):
+                       maps_out=None, band_timeout: float = 60.0, abort_group=None):
     """Body(frame) with its scales split across ranks; returns [(candidate, subset)] on `dst`
     (None elsewhere).  frame: uint8 [H,W,3] / [1,H,W,3] numpy, or a torch cuda tensor (then the
     maps stay on the device and travel over RCCL; with gloo they go through host memory).
@@ -236,8 +242,13 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
     sums each pixel in an order fixed by the layer and the scale's geometry (k slabs, DESIGN
     §4.1), so a band's rows and a scale on another rank equal the one-GPU network's maps, and the
     post path is the same code.
-    A rank whose piece fails aborts the band communicator (RCCL) or the process group (gloo)
-    before re-raising, so the ranks exchanging halos with it fail instead of waiting forever.
+    A band rank whose piece fails aborts its band communicator (RCCL) before re-raising; on the
+    RCCL path every band rank also waits for its exchanges for at most `band_timeout` seconds
+    (Handle.rccl_wait), so a neighbour of a failed rank aborts its own communicator and raises
+    TimeoutError instead of waiting forever.  gloo: a failing rank destroys the process group
+    (which releases its neighbours' pending send / recv) when `abort_group` is true; the default
+    is true only for an explicitly passed `group` -- the caller's WORLD group is left alone unless
+    asked.  KeyboardInterrupt / SystemExit are not band failures and abort nothing.
     maps_out: a list that receives the gathered per-scale maps on `dst` (tests)."""
     import numpy as np
     dev = hasattr(frame, "data_ptr")
@@ -277,10 +288,12 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
                 if on_device:  # RCCL: the library exchanges the halos itself
                     body.handle.set_band_peers(up, dn)
                     m = body.band_maps(local[0], s, r0, r1, "rccl")
+                    body.handle.rccl_wait(band_timeout)  # a neighbour that failed: abort, raise
                 else:
                     m = body.band_maps(local[0], s, r0, r1, band_exchange(up, dn, group))
-            except BaseException:
-                abort_band_group(body, group, on_device)
+            except Exception:
+                abort_band_group(body, group, on_device,
+                                 destroy_group=(group is not None) if abort_group is None else abort_group)
                 raise
         pieces[(s, owners[s].index(rank))] = m if on_device else torch.from_numpy(m)
     maps = [None] * len(geoms)

@@ -228,6 +228,9 @@ class _FakeHandle:
     def set_band_peers(self, up, dn):
         self.peers = (up, dn)
 
+    def rccl_wait(self, timeout_s):
+        pass
+
 
 class _FakeRcclBody(_FakeBody):
     """The device (RCCL) branch of body_scale_sharded: maps as tensors, bands through the
@@ -323,7 +326,8 @@ def _failing_worker(rank, world, port, q, bad):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=__import__("datetime").timedelta(seconds=600))
     try:
-        body_scale_sharded(_FailingBandBody(rank == bad), np.zeros((90, 160, 3), np.uint8), rank, world, split="balanced")
+        body_scale_sharded(_FailingBandBody(rank == bad), np.zeros((90, 160, 3), np.uint8), rank, world, split="balanced",
+                           abort_group=True)
         q.put((rank, "returned"))
     except BaseException as e:  # noqa: BLE001 -- reported to the parent
         q.put((rank, "raised: %s" % type(e).__name__))
@@ -334,8 +338,9 @@ def _failing_worker(rank, world, port, q, bad):
 
 def test_failed_band_rank_does_not_hang_its_neighbours():
     """one band rank raising mid-band used to leave its neighbours blocked in the
-    remaining halo exchanges until the backend timeout (10 min here).  body_scale_sharded now
-    aborts the group on the failing rank, so within seconds the failing rank re-raises its own
+    remaining halo exchanges until the backend timeout (10 min here).  With abort_group=True
+    (the caller's opt-in for its WORLD group) body_scale_sharded destroys the group on the failing
+    rank, so within seconds the failing rank re-raises its own
     error, its band neighbours raise, and no rank is left waiting."""
     import sys
     sys.path.insert(0, PKG)
@@ -357,3 +362,74 @@ def test_failed_band_rank_does_not_hang_its_neighbours():
     assert res[bad] == "raised: RuntimeError", res
     for r in banded[1:]:
         assert res[r].startswith("raised"), res
+
+
+class _DeadlineHandle(_FakeHandle):
+    """The library handle of a band rank whose neighbour failed: rccl_wait raises what the library
+    reports after its deadline (or an interrupt arrives while waiting)."""
+
+    def __init__(self, exc):
+        super().__init__()
+        self.exc, self.waits, self.aborts = exc, [], 0
+
+    def rccl_wait(self, timeout_s):
+        self.waits.append(timeout_s)
+        raise self.exc
+
+    def rccl_abort(self):
+        self.aborts += 1
+
+
+class _DeadlineBody(_FakeRcclBody):
+    def band_maps(self, frame, s, r0, r1, exchange=None):
+        assert exchange == "rccl"
+        self.bands.append((s, r0, r1, self.handle.peers))
+        return torch.zeros((1, 57, r1 - r0, GEOMS[s][1]))
+
+
+@pytest.mark.parametrize("exc,aborts", [(TimeoutError("no progress within the deadline"), 1),
+                                        (KeyboardInterrupt(), 0)])
+def test_rccl_band_neighbour_bounded_wait(monkeypatch, exc, aborts):
+    """on the RCCL path a failed rank's ncclCommAbort cannot cancel the recv kernels
+    queued on its neighbours' streams.  Every band rank therefore waits for its exchanges with
+    Handle.rccl_wait(band_timeout); when that reports the deadline (the library has then aborted
+    the rank's own communicator so its kernels exit), body_scale_sharded drops the communicator
+    and re-raises, leaving the torch process group alone.  An interrupt is not a band failure:
+    nothing is aborted."""
+    import sys
+    sys.path.insert(0, PKG)
+    from src import dist as sdist
+    destroyed = []
+    monkeypatch.setattr(sdist.dist, "get_backend", lambda group=None: "nccl")
+    monkeypatch.setattr(sdist.dist, "destroy_process_group", lambda group=None: destroyed.append(group))
+    monkeypatch.setattr(sdist, "init_band_comm", lambda body, group=None: None)
+    world = 4
+    _, owners, _ = sdist.split_plan([g[0] * g[1] for g in GEOMS], world, [g[0] for g in GEOMS])
+    rank = [rs for rs in owners if len(rs) > 1][0][1]  # a band with a neighbour above
+    body = _DeadlineBody()
+    body.handle = _DeadlineHandle(exc)
+    with pytest.raises(type(exc)):
+        sdist.body_scale_sharded(body, torch.zeros((90, 160, 3), dtype=torch.uint8), rank, world,
+                                 band_timeout=0.25)
+    assert body.handle.waits == [0.25] and len(body.bands) == 1
+    assert body.handle.aborts == aborts and destroyed == []
+
+
+def test_abort_band_group_leaves_world_group_unless_asked(monkeypatch):
+    """abort_band_group destroys a process group only on the gloo path and only when
+    the caller asks (body_scale_sharded asks for an explicitly passed band subgroup, or with
+    abort_group=True); the RCCL path never touches the torch process group."""
+    import sys
+    sys.path.insert(0, PKG)
+    from src import dist as sdist
+    destroyed = []
+    monkeypatch.setattr(sdist.dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(sdist.dist, "destroy_process_group", lambda group=None: destroyed.append(group))
+    body = _DeadlineBody()
+    body.handle = _DeadlineHandle(None)
+    sdist.abort_band_group(body, None)
+    sdist.abort_band_group(body, "sub", rccl=True, destroy_group=True)
+    assert destroyed == [] and body.handle.aborts == 1
+    sdist.abort_band_group(body, "sub", destroy_group=True)
+    sdist.abort_band_group(body, None, destroy_group=True)
+    assert destroyed == ["sub", None]

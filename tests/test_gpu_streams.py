@@ -156,6 +156,62 @@ def test_graph_replay_equals_eager():
         assert pk.dtype == ref_h.dtype and np.array_equal(pk, ref_h)
 
 
+def test_destroyed_handles_graphs_do_not_break_replays():
+    """handles with captured graphs are destroyed while others keep replaying
+    theirs (the round-4 crash: gpurun_out/c3d.log, a C5 handle's replay after another handle's
+    teardown).  Cause, reproduced without libopose by scripts/graph_fork_repro.hip: torch's
+    bundled HIP 7.0.2 runtime segfaults in hipGraphLaunch on forked graphs once other forked
+    executables are destroyed.  The library keeps every capture a single chain (run_graphed refuses
+    any other), so here: a lockstep two-scale Body, a one-scale Body, an OPOSE_LOCKSTEP=0 Body (its
+    scales fork eagerly onto pooled streams) and a Hand each capture; three of them are deleted in
+    turn, and the survivors replay 5x after each deletion with unchanged outputs; handles created
+    afterwards (reusing the pooled streams) capture and replay the same results."""
+    import gc
+    from src.body import Body
+    from src.hand import Hand
+    from src.weights import seeded_state_dict
+    rng = np.random.default_rng(25)
+    img = rng.integers(0, 256, (184, 232, 3), dtype=np.uint8)
+    crop = rng.integers(0, 256, (128, 128, 3), dtype=np.uint8)
+    bsd, hsd = seeded_state_dict("body", 0), seeded_state_dict("hand", 0)
+
+    def lockstep_off():
+        os.environ["OPOSE_LOCKSTEP"] = "0"
+        try:
+            return Body(bsd, scale_search=(0.5, 1.0))
+        finally:
+            del os.environ["OPOSE_LOCKSTEP"]
+
+    makers = {"pyr": lambda: Body(bsd, scale_search=(0.5, 1.0)), "one": lambda: Body(bsd),
+              "eager_fork": lockstep_off, "hand": lambda: Hand(hsd)}
+    inputs = {"pyr": img, "one": img, "eager_fork": img, "hand": crop}
+    hs = {k: m() for k, m in makers.items()}
+    ref = {}
+    for k, h in hs.items():
+        for _ in range(3):  # eager, capture, replay
+            ref[k] = h(inputs[k])
+
+    def same(k, out):
+        if k == "hand":
+            assert out.dtype == ref[k].dtype and np.array_equal(out, ref[k]), k
+        else:
+            assert np.array_equal(out[0], ref[k][0]) and np.array_equal(out[1], ref[k][1]), k
+
+    for victim in ("eager_fork", "pyr", "hand"):
+        del hs[victim]
+        gc.collect()
+        for _ in range(5):
+            for k, h in hs.items():
+                same(k, h(inputs[k]))
+    assert ref["pyr"][0].shape == ref["eager_fork"][0].shape
+    assert np.array_equal(ref["pyr"][0], ref["eager_fork"][0])  # lockstep == per-scale networks
+    for k in ("pyr", "hand", "eager_fork"):
+        h = makers[k]()
+        for _ in range(5):
+            same(k, h(inputs[k]))
+            same("one", hs["one"](img))
+
+
 def test_forward_waits_for_half_input(body):
     x = torch.from_numpy(np.random.default_rng(6).standard_normal((1, 3, 64, 96)).astype(np.float32))
     xh = x.half()
