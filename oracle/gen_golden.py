@@ -600,3 +600,56 @@ def gen_fullsize():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "fullsize":
     gen_fullsize()
+
+
+# ---------------------------------------------------------------- C2-size end to end + the reference's own tie noise
+def gen_e2e_c2():
+    """Verdict r4 item 6.  (a) C2's frame size, 368x656, through the reference's own Body() with
+    the seeded network at 8 torch threads (as every golden here): tests/golden/body_e2e_31_368x656.npz
+    (the image is regenerated from its seed).  (b) The reference against itself: every body_e2e
+    golden's image through the reference's Body() at 1, 2, 4, 8 and 16 threads, each run's keypoints
+    against the 8-thread golden, and whether every keypoint it moves sits on a float64 plateau
+    (oracle/ties.py) -> profiles/r5_ref_thread_noise.json."""
+    from src.model import bodypose_model
+    from oracle import ties
+    assert "reference" in sys.modules["src.model"].__file__
+    m = bodypose_model().eval()
+    sd = onet.seeded_state_dict("body", 0)
+    m.load_state_dict({k: sd[".".join(k.split(".")[1:])] for k in m.state_dict().keys()})
+    seed, hw = 31, (368, 656)
+    img31 = np.random.default_rng(seed).integers(0, 256, size=hw + (3,), dtype=np.uint8)
+    torch.set_num_threads(8)
+    cand, subset = ref_body(m)(img31)
+    name = f"body_e2e_{seed}_{hw[0]}x{hw[1]}.npz"
+    np.savez_compressed(os.path.join(OUT, name), img_seed=np.array(seed), img_hw=np.array(hw),
+                        img_sum=np.array(int(img31.astype(np.int64).sum())), candidate=cand, subset=subset)
+    print("wrote", name, cand.shape, subset.shape)
+    rows = []
+    for path in sorted(glob.glob(os.path.join(OUT, "body_e2e_*.npz"))):
+        d = np.load(path)
+        img = d["img"] if "img" in d else img31
+        up, blur = ties.f64_smoothed(img, sd)
+        for th in (1, 2, 4, 8, 16):
+            torch.set_num_threads(th)
+            c, s = ref_body(m)(img)
+            r = {"golden": os.path.basename(path), "threads": th, "keypoints": len(c),
+                 "people": len(s), "golden_people": len(d["subset"])}
+            if len(c) == len(d["candidate"]):
+                moved = int((c[:, :2] != d["candidate"][:, :2]).any(1).sum())
+                pairs = ties.tie_pairs(up, blur, c, d["candidate"])
+                r.update(moved_vs_8_threads=moved, moves_on_f64_ties=pairs is not None and len(pairs) == moved,
+                         identical_to_golden=bool(np.array_equal(c, d["candidate"]) and np.array_equal(s, d["subset"])))
+            rows.append(r)
+            print(json.dumps(r), flush=True)
+    torch.set_num_threads(8)
+    with open(os.path.join(REPO, "profiles", "r5_ref_thread_noise.json"), "w") as fh:
+        json.dump({"generator": "oracle/gen_golden.py e2e_c2", "reference": "src/body.py Body.__call__ with src/model.py "
+                   "bodypose_model (imported read-only), seeded weights", "torch": torch.__version__,
+                   "tie_rule": "oracle/ties.py: float64 smoothed values within 1e-6 of the part map's max", "rows": rows},
+                  fh, indent=1)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "e2e_c2":
+    install_shims()
+    sys.path.insert(0, REF)
+    gen_e2e_c2()

@@ -12,6 +12,17 @@ for p in (REPO, PKG):
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 
+def golden_image(d):
+    """The input image of a body_e2e fixture: stored, or regenerated from its seed (C2-size
+    fixtures keep only the seed and a checksum; oracle/gen_golden.py e2e_c2)."""
+    import numpy as np
+    if "img" in d:
+        return d["img"]
+    img = np.random.default_rng(int(d["img_seed"])).integers(0, 256, size=tuple(d["img_hw"]) + (3,), dtype=np.uint8)
+    assert int(img.astype(np.int64).sum()) == int(d["img_sum"])
+    return img
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libopose.so on cuda:0)")
     config.addinivalue_line("markers", "slow: long-running CPU test")

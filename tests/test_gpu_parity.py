@@ -15,7 +15,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import GOLDEN
+from conftest import GOLDEN, golden_image
 
 pytestmark = pytest.mark.gpu
 
@@ -194,64 +194,45 @@ def test_network_full_size_and_batch_vs_oracle():
     _net_tol(p2, paf[2:3])
 
 
-def _f64_tie_pairs(img, cand, ref_c):
-    """Rows where the GPU and the reference put a keypoint on different pixels, paired up: each
-    reference row with a GPU row one pixel away whose float64-network smoothed heat values (the
-    map the peak search runs on, src/body.py:76-80) differ by at most 1e-6 of that map's maximum
-    in some part -- a plateau the fp32 network noise (~5e-6 of the map range, either network)
-    may tip either way.  Returns {gpu row: reference row}, or None if a row is not such a move."""
-    from scipy.ndimage import gaussian_filter
-    from oracle import body_post, network
-    H, W = img.shape[:2]
-    x, pad, phw = body_post.preprocess(img, 0.5 * 368 / H)
-    sd = {k: v.double() for k, v in network.seeded_state_dict("body", 0).items()}
-    _, heat = network.body_forward(torch.from_numpy(x).double(), sd)
-    up = body_post.upsample_map(heat.float().numpy()[0], pad, phw, (H, W))  # [H, W, 19]
-    blur = [gaussian_filter(up[:, :, p].astype(np.float64), sigma=3) for p in range(18)]
-    gi = [i for i in range(len(cand)) if not np.array_equal(cand[i, :2], ref_c[i, :2])]
-    pairs = {}
-    for j in gi:
-        xr, yr = (int(v) for v in ref_c[j, :2])
-        hit = None
-        for i in gi:
-            xg, yg = (int(v) for v in cand[i, :2])
-            if i in pairs or abs(xg - xr) > 1 or abs(yg - yr) > 1 or not (0 <= xg < W and 0 <= yg < H):
-                continue
-            # the keypoint's part: the one whose map holds its score (the raw heat value) there
-            p = int(np.argmin(np.abs(up[yg, xg, :18] - cand[i, 2])))
-            if abs(up[yg, xg, p] - cand[i, 2]) > 1e-4 or abs(up[yr, xr, p] - ref_c[j, 2]) > 1e-4:
-                continue
-            if abs(blur[p][yg, xg] - blur[p][yr, xr]) <= 1e-6 * blur[p].max():
-                hit = i
-                break
-        if hit is None:
-            return None
-        pairs[hit] = j
-    return pairs
+# Keypoints the GPU may place on the other pixel of a float64 plateau (oracle/ties.py: smoothed
+# values within 1e-6 of the part map's max), per fixture -- the counts observed on hardware, never
+# more than the reference moves against itself at that size (profiles/r5_ref_thread_noise.json:
+# body_e2e_31 at 1 / 16 torch threads moves 4 / 2 of its own 1,350 keypoints, all onto such
+# plateaus; on body_e2e_21 / 22 it moves none).  Every other fixture: exact pixels.
+_TIE_ALLOWANCE = {"body_e2e_21_96x128.npz": 1, "body_e2e_31_368x656.npz": 4}
 
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "body_e2e_*.npz"))), ids=os.path.basename)
 def test_body_end_to_end_vs_reference(body, path):
-    """Full Body() on a random image with seeded weights against the reference's own run: the
-    north-star bar, identical keypoint pixels (coords within +-0.5 px, i.e. equal) and identical
-    person/subset assignment.  Network fp32 summation noise (the reference's torch-CPU order vs
-    the GPU's) can only tip exact plateaus of the smoothed heat map: a keypoint may sit one pixel
-    from the reference's where the float64 network's smoothed values of the two pixels agree to
-    1e-6 of the map (_f64_tie_pairs; body_e2e_21 has one, 2e-7 apart) -- its ids are then mapped,
-    and the people and their assignment must be identical."""
+    """Full Body() on a random image with seeded weights against the reference's own run (its
+    src/body.py Body.__call__ on src/model.py's network, 8 torch threads): the north-star bar,
+    identical keypoint pixels and identical person/subset assignment -- except on fixtures listed in
+    _TIE_ALLOWANCE, where at most that many keypoints may sit one pixel from the reference's on a
+    float64 plateau of the smoothed heat map (body_e2e_21: one, 2e-7 apart; the fp32 summation
+    order decides it, as the reference's own thread count does at C2's size).  Such keypoints' ids
+    are mapped; the people and their assignment must still be identical, and only the scores of
+    the people holding a moved keypoint may change beyond rtol 1e-3 (to 3e-2: the keypoint's heat
+    value and its limbs' PAF integrals move with it)."""
+    from oracle import ties
+    from oracle.network import seeded_state_dict as oracle_sd
     d = np.load(path)
-    cand, subset = body(d["img"])
+    img = golden_image(d)
+    cand, subset = body(img)
     ref_c, ref_s = d["candidate"], d["subset"]
     assert cand.shape == ref_c.shape
     ids = np.arange(len(cand), dtype=np.float64)
     moved = []  # reference ids of keypoints on another (tied) pixel
+    allowance = _TIE_ALLOWANCE.get(os.path.basename(path), 0)
     if not np.array_equal(cand[:, :2], ref_c[:, :2]):
-        pairs = _f64_tie_pairs(d["img"], cand, ref_c)
-        assert pairs is not None and len(pairs) <= 4, "keypoints moved away from float64 ties"
+        assert allowance, "keypoint pixels differ on a fixture with no tie allowance"
+        up, blur = ties.f64_smoothed(img, oracle_sd("body", 0))
+        pairs = ties.tie_pairs(up, blur, cand, ref_c)
+        assert pairs is not None, "keypoints moved away from float64 ties"
         for i, j in pairs.items():
             ids[i] = j
             if not np.array_equal(cand[i, :2], ref_c[j, :2]):
                 moved.append(j)
+        assert len(moved) <= allowance, (len(moved), allowance)
         keep = np.setdiff1d(np.arange(len(cand)), list(pairs))
         assert np.array_equal(cand[keep, :2], ref_c[keep, :2])
         np.testing.assert_allclose(cand[keep, 2], ref_c[keep, 2], rtol=1e-3, atol=1e-4)
@@ -261,8 +242,6 @@ def test_body_end_to_end_vs_reference(body, path):
     assert subset.shape == ref_s.shape
     mapped = np.where(subset[:, :18] >= 0, ids[np.maximum(subset[:, :18], 0).astype(int)], -1)
     assert np.array_equal(mapped, ref_s[:, :18]) and np.array_equal(subset[:, 19], ref_s[:, 19])
-    # a person's score sums its keypoints' raw heat values and its limbs' PAF integrals: a tied
-    # keypoint one pixel over changes both (body_e2e_21: 3.2430 -> 3.2968)
     touched = np.isin(ref_s[:, :18], moved).any(1)
     np.testing.assert_allclose(subset[~touched, 18], ref_s[~touched, 18], rtol=1e-3)
     np.testing.assert_allclose(subset[touched, 18], ref_s[touched, 18], rtol=3e-2)

@@ -71,7 +71,7 @@ def test_records_pipelined(body, batches, expected):
 
 @pytest.mark.parametrize("mix", ["defer_only", "mixed"])
 def test_records_pipelined_deferred(body, batches, expected, mix):
-    """pipeline="defer" (OPOSE_PIPELINE_DEFER, bench.py's default): each call's post-processing
+    """pipeline="defer" (OPOSE_PIPELINE_DEFER; opt-in, bench.py with BENCH_DEFER=1): each call's post-processing
     is enqueued by the next call once its network reaches conv3_1 (or by flush / synchronize /
     decode_records / any other entry point).  Every record equals the host path's, whether the
     deferred calls run back to back, alternate with plain pipelined calls, or are followed by a

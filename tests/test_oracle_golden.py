@@ -10,7 +10,7 @@ import torch
 from oracle import body_post, hand_post, network
 from oracle.cv_resize import cubic_coeffs, resize_cubic
 
-from conftest import GOLDEN
+from conftest import GOLDEN, golden_image
 
 
 def _files(pat):
@@ -72,7 +72,12 @@ def test_body_end_to_end_matches_reference(path):
         p, h = network.body_forward(torch.from_numpy(x), sd)
         return p.numpy(), h.numpy()
 
-    cand, subset = body_post.body_infer(d["img"], net_fn)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(8)  # the goldens' thread count (the reference's order depends on it)
+    try:
+        cand, subset = body_post.body_infer(golden_image(d), net_fn)
+    finally:
+        torch.set_num_threads(nt)
     assert np.array_equal(cand, d["candidate"])
     assert np.array_equal(subset, d["subset"])
 
