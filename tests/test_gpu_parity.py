@@ -195,11 +195,11 @@ def test_network_full_size_and_batch_vs_oracle():
 
 
 # Keypoints the GPU may place on the other pixel of a float64 plateau (oracle/ties.py: smoothed
-# values within 1e-6 of the part map's max), per fixture -- the counts observed on hardware, never
+# values within 1e-6 of the part map's max), per fixture -- the counts observed on hardware (round 5), never
 # more than the reference moves against itself at that size (profiles/r5_ref_thread_noise.json:
 # body_e2e_31 at 1 / 16 torch threads moves 4 / 2 of its own 1,350 keypoints, all onto such
 # plateaus; on body_e2e_21 / 22 it moves none).  Every other fixture: exact pixels.
-_TIE_ALLOWANCE = {"body_e2e_21_96x128.npz": 1, "body_e2e_31_368x656.npz": 4}
+_TIE_ALLOWANCE = {"body_e2e_21_96x128.npz": 1, "body_e2e_31_368x656.npz": 3}
 
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "body_e2e_*.npz"))), ids=os.path.basename)
@@ -232,6 +232,7 @@ def test_body_end_to_end_vs_reference(body, path):
             ids[i] = j
             if not np.array_equal(cand[i, :2], ref_c[j, :2]):
                 moved.append(j)
+        print(f"{os.path.basename(path)}: {len(moved)} keypoint(s) across float64 plateaus (allowed {allowance})")
         assert len(moved) <= allowance, (len(moved), allowance)
         keep = np.setdiff1d(np.arange(len(cand)), list(pairs))
         assert np.array_equal(cand[keep, :2], ref_c[keep, :2])
