@@ -183,7 +183,11 @@ def test_rccl_exchange_moves_the_halo_rows(bodies, frame):
     ref = ref_body.band_maps(frame, 3, 30, 60, self_copy)
     assert np.array_equal(got, ref)
     dev = b.band_maps(torch.from_numpy(frame).cuda(), 3, 30, 60, "rccl")
+    b.handle.rccl_wait(30.0)  # the exchanges completed: the bounded wait returns, nothing aborted
     assert np.array_equal(dev.cpu().numpy(), ref)
+    dev2 = b.band_maps(torch.from_numpy(frame).cuda(), 3, 30, 60, "rccl")  # the communicator is still up
+    b.handle.rccl_wait(30.0)
+    assert np.array_equal(dev2.cpu().numpy(), ref)
     b.handle.set_band_peers(None, None)
 
 
