@@ -1038,8 +1038,14 @@ static int slab_count(opose_ctx* h, const DevConv* c, bool win, int N, int H, in
         if (pool) return 1;
         // the 7x7 stages, and conv5_3_CPM (3x3, 128 outputs: 62 whole tiles for a 368 crop)
         if (!(c->ks == 7 && win) && !(c->ks == 3 && c->Mpad <= 128)) return 1;
+        // A 368 crop's scales have 3 / 9 / 19 / 34 tiles: 4 / 7 / 8 / 4 slabs make 363 units whose
+        // longest-first packing over 256 workgroups is within a chunk of the best of every table of
+        // 1-16 slabs per scale (a makespan model with a per-unit overhead of 4 chunks), with the
+        // fewest units of those (fewer partials, a shorter fixup).  Measured, same box: one crop
+        // 7.39-7.53 -> 7.09 ms, a 368 + 256 crop batch 13.85-13.97 -> 13.50 ms (round 4's
+        // 16 / 12 / 8 / 7; profiles/r5_hand_slabs.log).
         const double T = std::ceil(npix / 256.0) * mr;
-        return clampS(T < 6 ? 16 : T < 12 ? 12 : T < 30 ? 8 : T < 60 ? 7 : T < 120 ? 4 : T < 240 ? 2 : 1);
+        return clampS(T < 6 ? 4 : T < 12 ? 7 : T < 30 ? 8 : T < 60 ? 4 : T < 120 ? 4 : T < 240 ? 2 : 1);
     }
     const int mult = c->pair ? 2 : 1;
     if (std::ceil(npix / 256.0) * mr * mult >= 160) return 1;  // the bench's batches: whole tiles fill the chip
