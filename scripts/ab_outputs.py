@@ -33,6 +33,11 @@ def save(path):
         paf, heat = body(x)
         out["body%d_paf" % n] = paf
         out["body%d_heat" % n] = heat
+    # the bench's layer shapes: 8 frames at the network input of a 368x656 frame at scale 0.5
+    x = rng.standard_normal((8, 3, 184, 328)).astype(np.float32) * 0.5
+    paf, heat = body(x)
+    out["body8s_paf"] = paf
+    out["body8s_heat"] = heat
     np.savez(path, **out)
     print("saved", path, {k: v.shape for k, v in out.items()})
 
