@@ -929,7 +929,8 @@ static XAct frame_view(const XAct& a, int n, int H, int W) {
 //    one segment per frame (frame views of the same buffers; a crop batch's 92 x 92 scale);
 //  * body layers of fewer than 4096 pixels (C2's single frame, a pyramid's 0.5 scale): conv_x6,
 //    whose 128 x 64 tiles spread a small layer over the chip;
-//  * the hand's 512-channel 3x3 layers at H/8 (conv4_x, conv5_x): conv_x6, whose 256 x 128 tiles
+//  * the hand's 512-channel 3x3 layers at H/8 (conv4_x, conv5_1/5_2; not conv5_3_CPM's 128 outputs,
+//    which take the 7x7 layers' slab layout on the window kernel): conv_x6, whose 256 x 128 tiles
 //    cover a 368 crop's 4-scale pyramid in one data-parallel round (254 tiles; the window
 //    kernel's 128 x 256 tiles make 260: 225 vs 270 TF/s);
 //  * everything else (dense inputs, pooled convs, 1x1): conv_x6.
@@ -939,7 +940,7 @@ static int seg_kernel(const opose_ctx* h, const ConvSeg& sg, bool pool) {
     if (!h->win7 || pool || !c->wx6p || !sg.in.padded || (c->ks != 3 && c->ks != 7)) return kKernelX6;
     const long lpix = (long)sg.N * (sg.Hl ? sg.Hl : sg.H) * sg.W;
     if (c->net == OPOSE_NET_BODY && lpix < 4096) return kKernelX6;
-    if (c->net == OPOSE_NET_HAND && c->ks == 3 && c->lvl == 3) return kKernelX6;
+    if (c->net == OPOSE_NET_HAND && c->ks == 3 && c->lvl == 3 && c->Mpad > 128) return kKernelX6;
     if (sg.N == 1) return conv_win_fits_rows(sg.W, c->ks) ? kKernelWin : kKernelX6;
     if (conv_win_fits(sg.N, sg.H, sg.W, c->ks)) return kKernelWin;
     if (c->ks == 7 && h->split_frames && conv_win_fits_rows(sg.W, c->ks)) return kKernelWinFrames;
@@ -1036,8 +1037,9 @@ static int slab_count(opose_ctx* h, const DevConv* c, bool win, int N, int H, in
     auto clampS = [&](long s) { return (int)std::max<long>(1, std::min<long>(s, smax)); };
     if (c->net == OPOSE_NET_HAND) {
         if (pool) return 1;
-        // the 7x7 stages, and conv5_3_CPM (3x3, 128 outputs: 62 whole tiles for a 368 crop)
-        if (!(c->ks == 7 && win) && !(c->ks == 3 && c->Mpad <= 128)) return 1;
+        // the 7x7 stages, and conv5_3_CPM (3x3 at H/8, 128 outputs: 65 whole tiles for a 368 crop);
+        // conv2_1 (128 outputs at H/2: 994 tiles) runs whole tiles
+        if (!(c->ks == 7 && win) && !(c->ks == 3 && c->Mpad <= 128 && c->lvl == 3)) return 1;
         // A 368 crop's scales have 3 / 9 / 19 / 34 tiles: 4 / 7 / 8 / 4 slabs make 363 units whose
         // longest-first packing over 256 workgroups is within a chunk of the best of every table of
         // 1-16 slabs per scale (a makespan model with a per-unit overhead of 4 chunks), with the
