@@ -1251,19 +1251,21 @@ struct ChainSeg {
 static void run_chain_x6(opose_ctx* h, const std::vector<ChainSeg>& segs) {
     // a small frame's 512-wide stage-1 pair (C2: 943 pixels, 15 workgroups of 64 pixels per
     // branch in the fused kernel, 42 us) runs as two launches over 128 x 64 tiles: the same sums
-    // (1x1 convs never split k, the fused kernel rounds the intermediate like conv_x6's epilogue)
+    // (1x1 convs never split k, the fused kernel rounds the intermediate like conv_x6's epilogue).
+    // Not a hand pyramid's small scales: they share the fused launch of the large ones.
+    auto small_pair = [&](const ChainSeg& sg) {
+        return (long)sg.N * (sg.Hl ? sg.Hl : sg.H) * sg.W <= 4096 && sg.c1->cout >= 256 && sg.c1->net == OPOSE_NET_BODY;
+    };
     {
         std::vector<ChainSeg> small, rest;
-        for (const ChainSeg& sg : segs)
-            ((long)sg.N * (sg.Hl ? sg.Hl : sg.H) * sg.W <= 4096 && sg.c1->cout >= 256 ? small : rest).push_back(sg);
+        for (const ChainSeg& sg : segs) (small_pair(sg) ? small : rest).push_back(sg);
         if (!small.empty() && !rest.empty()) {
             run_chain_x6(h, small);
             run_chain_x6(h, rest);
             return;
         }
     }
-    bool fuse = h->fuse1x1 && !segs.empty() && segs.size() <= (size_t)kX6Groups &&
-                !((long)segs[0].N * (segs[0].Hl ? segs[0].Hl : segs[0].H) * segs[0].W <= 4096 && segs[0].c1->cout >= 256);
+    bool fuse = h->fuse1x1 && !segs.empty() && segs.size() <= (size_t)kX6Groups && !small_pair(segs[0]);
     for (const ChainSeg& sg : segs) {
         const DevConv *c1 = sg.c1, *c2 = sg.c2;
         fuse = fuse && c1->ks == 1 && c2->ks == 1 && c1->cin_g == 16 && c1->cout == c1->Mpad && c1->Mpad % 128 == 0 &&
@@ -1994,7 +1996,21 @@ static void body_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
         h->prof_end(pe);
     } else {
     double* avg = h->avg.ensure<double>((size_t)N * 18 * H * W, h->stream);
-    for (int s = 0; s < ns; ++s) {
+    HeatScales hsc{};
+    hsc.n = ns;
+    hsc.ns = (float)ns;
+    double mid_bytes = 0;
+    for (int s = 0; s < ns && s < kHeatScales; ++s) {
+        hsc.s[s] = HeatScale{S.mid[s], 18, 0, gs[s].Hs, gs[s].Ws, gs[s].up_sy, gs[s].up_sx};
+        mid_bytes += (double)N * 18 * 4.0 * gs[s].Hs * gs[s].Ws;
+    }
+    const bool fused_avg = !f32 && heat_full_scales_fits(hsc, H, W);  // several scales: one launch
+    if (fused_avg) {
+        h->prof_begin(pe, "heat_full", 0, (double)N * 18 * H * W * 8.0 + mid_bytes);
+        launch_heat_full_scales(hsc, N, 18, H, W, avg, h->stream);
+        h->prof_end(pe);
+    }
+    for (int s = 0; s < ns && !fused_avg; ++s) {
         h->prof_begin(pe, "heat_full", 0,
                       (double)N * 18 * (H * W * (f32 ? 4.0 : 8.0) * (s ? 2 : 1) + 4.0 * gs[s].Hs * gs[s].Ws));
         if (f32)
@@ -3053,12 +3069,27 @@ static void hand_post_common(opose_ctx* h, int N, int H, int W, const std::vecto
     const int NP = N * 21;
     double* avg = h->avg.ensure<double>((size_t)NP * H * W, h->stream);
     ProfEntry pe;
-    for (int s = 0; s < ns; ++s) {
-        h->prof_begin(pe, "heat_full", 0, (double)NP * H * W * 8 * (s ? 2 : 1));
-        const float* mid = h->mid(s).ensure<float>(0, h->stream) + (size_t)mid_crop * 21 * gs[s].Hs * gs[s].Ws;
-        launch_heat_full(mid, 21, 0, 21, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx, ns, s > 0, avg,
-                         h->stream);
+    HeatScales hsc{};
+    hsc.n = ns;
+    hsc.ns = (float)ns;
+    double mid_bytes = 0;
+    for (int s = 0; s < ns && s < kHeatScales; ++s) {
+        hsc.s[s] = HeatScale{h->mid(s).ensure<float>(0, h->stream) + (size_t)mid_crop * 21 * gs[s].Hs * gs[s].Ws, 21, 0,
+                             gs[s].Hs, gs[s].Ws, gs[s].up_sy, gs[s].up_sx};
+        mid_bytes += (double)NP * 4.0 * gs[s].Hs * gs[s].Ws;
+    }
+    if (heat_full_scales_fits(hsc, H, W)) {  // every scale in one launch, the average written once
+        h->prof_begin(pe, "heat_full", 0, (double)NP * H * W * 8 + mid_bytes);
+        launch_heat_full_scales(hsc, N, 21, H, W, avg, h->stream);
         h->prof_end(pe);
+    } else {
+        for (int s = 0; s < ns; ++s) {
+            h->prof_begin(pe, "heat_full", 0, (double)NP * H * W * 8 * (s ? 2 : 1));
+            const float* mid = h->mid(s).ensure<float>(0, h->stream) + (size_t)mid_crop * 21 * gs[s].Hs * gs[s].Ws;
+            launch_heat_full(mid, 21, 0, 21, N, gs[s].Hs, gs[s].Ws, H, W, gs[s].up_sy, gs[s].up_sx, ns, s > 0, avg,
+                             h->stream);
+            h->prof_end(pe);
+        }
     }
     int* lab = h->hlab.ensure<int>((size_t)NP * H * W, h->stream);
     double* sums = h->hsums.ensure<double>((size_t)NP * H * W, h->stream);

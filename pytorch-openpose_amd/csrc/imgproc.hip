@@ -168,6 +168,87 @@ __global__ __launch_bounds__(256) void cubic_resize_rows(const float* __restrict
     }
 }
 
+// All scales of a pyramid in one pass (src/body.py:51-67 and src/hand.py:43-56: for every m,
+// heatmap_avg += cv2.resize(x8 map, (W, H)) / len(multiplier)): per scale the row-staged resize
+// above, into a float64 register accumulator per output row, added in scale order from 0.0 --
+// the float64 sums launch_heat_full's per-scale launches store and re-read, with one write of the
+// average instead of a read-modify-write per scale.  A scale whose x8 map already has the output
+// size is read directly (cv2.resize copies).
+template <int MAXR>
+__global__ __launch_bounds__(256) void heat_full_scales(HeatScales S, int P, int H, int W, double* __restrict__ avg) {
+    __shared__ float hs[MAXR][256];
+    __shared__ CubicTap s_ty[RS_RT];
+    const int tid = threadIdx.x;
+    const int x = blockIdx.x * 256 + tid;
+    const int y0 = blockIdx.y * RS_RT;
+    const int y1 = min(y0 + RS_RT, H);
+    const int nc = blockIdx.z;
+    const int n = nc / P, c = nc - n * P;
+    const bool live = x < W;
+    double acc[RS_RT];
+#pragma unroll
+    for (int r = 0; r < RS_RT; ++r) acc[r] = 0.0;
+    for (int s = 0; s < S.n; ++s) {
+        const HeatScale& g = S.s[s];
+        const float* plane = g.mid + ((size_t)n * g.Cm + g.coff + c) * g.Hs * g.Ws;
+        const bool div = S.ns != 1.f;
+        if (g.Hs == H && g.Ws == W) {  // identity: the map itself
+            if (live) {
+#pragma unroll
+                for (int r = 0; r < RS_RT; ++r)
+                    if (y0 + r < y1) {
+                        const float o = plane[(size_t)(y0 + r) * W + x];
+                        const float v = div ? o / S.ns : o;
+                        acc[r] = acc[r] + (double)v;
+                    }
+            }
+            continue;
+        }
+        const int r_lo = cubic_tap(y0, g.sy, g.Hs).i[0];
+        const int r_hi = cubic_tap(y1 - 1, g.sy, g.Hs).i[3];
+        __syncthreads();  // the previous scale's staged rows are consumed
+        if (tid < y1 - y0) s_ty[tid] = cubic_tap(y0 + tid, g.sy, g.Hs);
+        if (live) {
+            const CubicTap tx = cubic_tap(x, g.sx, g.Ws);
+            for (int k0 = 0; k0 < MAXR && r_lo + k0 <= r_hi; k0 += RS_CHUNK) {
+                float q[RS_CHUNK][4];
+#pragma unroll
+                for (int k = 0; k < RS_CHUNK; ++k) {
+                    const float* row = plane + (size_t)min(r_lo + k0 + k, r_hi) * g.Ws;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) q[k][j] = row[tx.i[j]];
+                }
+#pragma unroll
+                for (int k = 0; k < RS_CHUNK; ++k) {
+                    float v = q[k][0] * tx.c[0];
+                    v = v + q[k][1] * tx.c[1];
+                    v = v + q[k][2] * tx.c[2];
+                    v = v + q[k][3] * tx.c[3];
+                    if (k0 + k < MAXR && r_lo + k0 + k <= r_hi) hs[k0 + k][tid] = v;
+                }
+            }
+        }
+        __syncthreads();
+        if (live) {
+#pragma unroll
+            for (int r = 0; r < RS_RT; ++r)
+                if (y0 + r < y1) {
+                    const CubicTap ty = s_ty[r];
+                    float o = hs[ty.i[0] - r_lo][tid] * ty.c[0];
+                    o = o + hs[ty.i[1] - r_lo][tid] * ty.c[1];
+                    o = o + hs[ty.i[2] - r_lo][tid] * ty.c[2];
+                    o = o + hs[ty.i[3] - r_lo][tid] * ty.c[3];
+                    const float v = div ? o / S.ns : o;
+                    acc[r] = acc[r] + (double)v;
+                }
+        }
+    }
+    if (!live) return;
+#pragma unroll
+    for (int r = 0; r < RS_RT; ++r)
+        if (y0 + r < y1) avg[((size_t)nc * H + y0 + r) * W + x] = acc[r];
+}
+
 // staged rows needed by one workgroup for a source step `scale` (destination -> source)
 static bool rows_fit(double scale) { return RS_RT * scale + 5.0 <= (double)RS_MAXR; }
 
@@ -210,6 +291,18 @@ void launch_heat_full(const float* mid, int Cm, int coff, int P, int N, int Hs, 
     dim3 grid((W + 255) / 256, H, N * P);
     hipLaunchKernelGGL(heat_full_accum<double>, grid, dim3(256), 0, st, mid, Cm, coff, P, Hs, Ws, H, W, sy, sx,
                        (float)nscales, accumulate, avg);
+}
+
+bool heat_full_scales_fits(const HeatScales& S, int H, int W) {
+    for (int s = 0; s < S.n; ++s)
+        if (!((S.s[s].Hs == H && S.s[s].Ws == W) || rows_fit(S.s[s].sy))) return false;
+    return S.n >= 1 && S.n <= kHeatScales;
+}
+
+void launch_heat_full_scales(const HeatScales& S, int N, int P, int H, int W, double* avg, hipStream_t st) {
+    if (!heat_full_scales_fits(S, H, W)) throw std::invalid_argument("heat_full_scales: scale out of range");
+    dim3 grid((W + 255) / 256, (H + RS_RT - 1) / RS_RT, N * P);
+    hipLaunchKernelGGL(heat_full_scales<RS_MAXR>, grid, dim3(256), 0, st, S, P, H, W, avg);
 }
 
 void launch_heat_full_f32(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,

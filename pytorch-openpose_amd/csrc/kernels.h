@@ -95,6 +95,20 @@ void launch_upsample8(const float* in, int in_cstride, int in_coff, int C, int N
                       float* out, hipStream_t st);
 void launch_heat_full(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
                       double sx, int nscales, int accumulate, double* avg, hipStream_t st);
+// every scale of a pyramid's heat average in one launch (imgproc.hip heat_full_scales)
+constexpr int kHeatScales = 8;
+struct HeatScale {
+    const float* mid;  // [N][Cm][Hs][Ws] x8 maps of this scale
+    int Cm, coff, Hs, Ws;
+    double sy, sx;
+};
+struct HeatScales {
+    HeatScale s[kHeatScales];
+    int n;
+    float ns;  // len(multiplier): every scale's map is divided by it (float32) before the float64 add
+};
+bool heat_full_scales_fits(const HeatScales& S, int H, int W);
+void launch_heat_full_scales(const HeatScales& S, int N, int P, int H, int W, double* avg, hipStream_t st);
 void launch_heat_full_f32(const float* mid, int Cm, int coff, int P, int N, int Hs, int Ws, int H, int W, double sy,
                           double sx, float* avg, hipStream_t st);
 
