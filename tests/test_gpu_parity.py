@@ -92,11 +92,10 @@ def test_preprocess_bit_exact(native, handle):
     # (H, W, scale_search entry); multiplier = s * 368 / H as src/body.py:32
     for (H, W, s) in [(368, 656, 0.5), (240, 320, 0.5), (97, 131, 1.0), (1080, 1920, 1.5),
                       (368, 368, 1.0), (100, 180, 2.0), (53, 97, 0.5),
-                      # C5's smallest scale (one output row per workgroup) and a source step so
-                      # large that a workgroup's byte run exceeds the LDS stage (global gather)
+                      # C5's smallest scale (a 5.9x source step) and a 41x source step
                       (1080, 1920, 0.5), (1500, 2999, 0.1),
-                      # frames whose byte size is a whole number of pages: the staged rows must
-                      # not read past the buffer's last byte
+                      # frames whose byte size is a whole number of pages (no slack after the
+                      # buffer's last byte)
                       (128, 128, 1.0), (256, 256, 0.5)]:
         img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
         hw = np.zeros(2, np.int32)
