@@ -54,6 +54,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     // barrier, so a stage has NST - 1 chunks to land
     static_assert(NST == 2 || NST == 3, "conv_win_x6 stages");
     constexpr int WOFF = NST * A_U;              // window buffers after the weight stages
+    static_assert(TM * TN >= 3, "block 4 hosts the offset steps");
 
     __shared__ __attribute__((aligned(16))) uint4 lds[NST * A_U + 2 * WBUF];
     __shared__ float s_bias[MT];
@@ -140,20 +141,30 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
         const int wpos = (3 + n * (H + 3) + y) * P + 3 + x - ws;
         bbase[j] = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + WOFF + wpos);
     }
-    // pair of this lane's k-group in a chunk: q = 4c + gi -> (group g, tap t), advanced by 4 per chunk
+    // pair of this lane's k-group in a chunk: q = 4c + gi -> (group g, tap t), advanced by 4 per
+    // chunk.  Chunk c + 1's fragment offsets are needed at chunk c's top; they are computed one
+    // chunk ahead in OFF_STEPS pieces, one per MFMA gap of block 4, off the chunk's critical path
+    // (computed at the chunk's top, their VALU chain delayed block 0: 7x7 launch 0.357 -> 0.353 ms)
     int pg_g = (4 * c_begin + gi) / TAPS, pg_t = (4 * c_begin + gi) % TAPS;  // chunk c_begin
-    auto pair_off = [&]() __attribute__((always_inline)) -> uint32_t {
-        const int g = min(pg_g, cin_g - 1);  // padded pairs past the last group: its data (weights 0)
-        const int ky = pg_t / KS;
-        const int shift = (ky - PAD) * P + (pg_t - ky * KS - PAD);
-        return (uint32_t)((g & 1) * WBUF * 16 + shift * 16);
-    };
-    auto advance = [&]() __attribute__((always_inline)) {
-        pg_t += 4;
-        if (pg_t >= TAPS) {
-            pg_t -= TAPS;
-            ++pg_g;
+    int s_dy = 0, s_dx = 0;
+    uint32_t off_n = 0;
+    constexpr int OFF_STEPS = 3;
+    auto off_step = [&](int k) __attribute__((always_inline)) {
+        if (k == 0) {
+            s_dy = pg_t / KS;
+            s_dx = pg_t - s_dy * KS - PAD;
+            s_dy -= PAD;
+        } else if (k == 1) {  // padded pairs past the last group: its data (weights 0)
+            off_n = (uint32_t)((min(pg_g, cin_g - 1) & 1) * WBUF * 16 + (s_dy * P + s_dx) * 16);
+        } else {  // advance to the next chunk's pair (branch-free)
+            const int w = pg_t + 4 >= TAPS ? 1 : 0;
+            pg_t = pg_t + 4 - w * TAPS;
+            pg_g += w;
         }
+    };
+    auto off_all = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < OFF_STEPS; ++k) off_step(k);
     };
 
     f32x4 acc[TM][TN];
@@ -208,9 +219,10 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
     __syncthreads();  // both windows and every stage landed everywhere
     uint32_t bcur[TN], bnxt[TN];
     {
-        const uint32_t off = pair_off();
+        off_all();  // chunk c_begin
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bnxt[j] = bbase[j] + off;  // chunk 0
+        for (int j = 0; j < TN; ++j) bnxt[j] = bbase[j] + off_n;  // chunk 0
+        off_all();  // chunk c_begin + 1, read at the first chunk's top
         const uint32_t a0 = la(0);
 #pragma unroll
         for (int r = 0; r < TMN; ++r) rd(0, r, a0, bnxt);
@@ -227,12 +239,8 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
         const int c2 = min(c + NST, c_end - 1);  // past the end: a harmless reload of the last chunk
 #pragma unroll
         for (int j = 0; j < TN; ++j) bcur[j] = bnxt[j];
-        advance();  // (pg_g, pg_t) -> chunk c + 1
-        {
-            const uint32_t off = pair_off();
 #pragma unroll
-            for (int j = 0; j < TN; ++j) bnxt[j] = bbase[j] + off;
-        }
+        for (int j = 0; j < TN; ++j) bnxt[j] = bbase[j] + off_n;  // chunk c + 1 (computed in chunk c - 1)
         // block 0 (needs R0): R2 of this chunk interleaved
         asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TMN > 15 ? 15 : TMN) : "memory");
         fence_all();
@@ -297,6 +305,7 @@ __global__ __launch_bounds__(64 * x6_waves(MT, PT), 1) void conv_win_x6(X6Args a
             constexpr int N4 = A_PW - 2;
 #pragma unroll
             for (int o = q * N4 / NB; o < (q + 1) * N4 / NB; ++o) dma_a_unit(c2, buf, 1 + o);
+            if (q < OFF_STEPS) off_step(q);  // chunk c + 2's offsets
             __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
@@ -410,7 +419,7 @@ void x6_pack_weights_pairs(const float* w, int cout, int cin, int ks, int Mpad, 
 }
 
 // window capacities (units per (piece, group)): LDS = 3 weight stages (72 KB) + 2 x 3 x 832 units
-// (78 KB; the bench's 23 x 41 frames at P = 57: <= 801 units), or 2 stages + 2 x 3 x 1088 units
+// (78 KB; the bench's 23 x 41 frames at P = 44: <= 707 units), or 2 stages + 2 x 3 x 1088 units
 constexpr int kWinSmall = 832, kWinLarge = 1088;
 constexpr int kWinStagesSmall = 3;  // weight stages of the small-window kernels (2: 2,021 vs 2,048 frames/s)
 
