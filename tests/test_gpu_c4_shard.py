@@ -145,8 +145,8 @@ def test_c4_shard_end_to_end_vs_oracle(records, frames_np, f):
     its 8- vs 1-thread runs disagree on 12.4 % on average, scripts/fp32_thread_noise.py).  The bar
     is the float64 network's keypoints: each GPU keypoint at a float64 keypoint's pixel or tipped
     across a plateau (smoothed values within 1e-5 of the map, _keypoints_vs_f64), none elsewhere,
-    and the people count within one of the float64 answer (a tipped keypoint changes limb scores,
-    and torch-fp32 itself differs by one person on frame 31)."""
+    and the float64 answer's people count -- on frame 31 within one (a tipped keypoint changes
+    limb scores: torch-fp32 itself differs by one person there, and so does the GPU, 22 vs 21)."""
     from oracle import network
     from src.weights import BENCH_OUT_SCALE
     sd64 = {k: v.double() for k, v in network.seeded_state_dict("body", 0, out_scale=BENCH_OUT_SCALE).items()}
@@ -155,7 +155,7 @@ def test_c4_shard_end_to_end_vs_oracle(records, frames_np, f):
     print(f"frame {f}: {len(cand)} GPU keypoints vs {n64} float64: {exact} exact, {tied} on plateaus, {bad} off; "
           f"people {len(subset)} vs {people64}")
     assert bad == 0 and len(cand) <= n64 + tied
-    assert abs(len(subset) - people64) <= 1
+    assert abs(len(subset) - people64) <= {0: 0, 31: 1}[f]
 
 
 def test_c4_shard_network_maps_vs_oracle(gpu_maps, frames_np):
