@@ -908,14 +908,6 @@ __global__ __launch_bounds__(256) void limb_greedy(const double* __restrict__ sc
     if (tid == 0) conn_cnt[nk] = count;
 }
 
-// uniform copy of lane `l`'s value (l wave-uniform)
-__device__ __forceinline__ double lane_value(double v, int l) {
-    const uint64_t u = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-
 // One wavefront per frame: sequential person assembly with lane-parallel row scans.  Every
 // limb's connections (score, both candidates' scores, candidate indices) are staged into LDS in
 // one parallel pass when they fit `stage` entries (the serial loop then reads LDS only, and the
@@ -986,41 +978,21 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
             for (int c = lane; c < nc; c += 64) stage_one(k, c, c);
             __syncthreads();
         }
-        // connection c0 + 1's staged values are loaded while c0's rows are scanned, and the scan
-        // also reads every row's ib / 18 / 19 columns, so row j1's update needs no further LDS
-        // round trip (its values come from the scanning lane by readlane)
-        double nA = 0.0, nB = 0.0, nS = 0.0, nSA = 0.0, nSB = 0.0;
-        auto load_conn = [&](int c) __attribute__((always_inline)) {
-            nA = (double)s_ci[2 * c];
-            nB = (double)s_ci[2 * c + 1];
-            nS = s_cs[c];
-            nSA = s_sa[c];
-            nSB = s_sb[c];
-        };
-        if (nc > 0) load_conn(base);
         for (int c0 = 0; c0 < nc; ++c0) {
-            const double idA = nA, idB = nB, s = nS, sa = nSA, sb = nSB;
-            if (c0 + 1 < nc) load_conn(base + c0 + 1);
+            const int c = base + c0;
+            const double idA = (double)s_ci[2 * c];
+            const double idB = (double)s_ci[2 * c + 1];
+            const double s = s_cs[c];
             int found = 0, j1 = -1, j2 = -1;
-            double j1b = 0.0, j1t = 0.0, j1n = 0.0;  // row j1's columns ib, 18, 19
             for (int r0 = 0; r0 < nrows; r0 += 64) {
                 const int r = r0 + lane;
-                const bool live = r < nrows;
-                const double va = live ? s_sub[r * 20 + ia] : 0.0, vb = live ? s_sub[r * 20 + ib] : 0.0;
-                const double vt = live ? s_sub[r * 20 + 18] : 0.0, vn = live ? s_sub[r * 20 + 19] : 0.0;
-                const bool hit = live && (va == idA || vb == idB);
-                unsigned long long bm = __ballot(hit);
-                while (bm && found < 3) {
-                    const int bit = __ffsll((long long)bm) - 1;
-                    bm &= bm - 1;
-                    if (found == 0) {
-                        j1 = r0 + bit;
-                        j1b = lane_value(vb, bit);
-                        j1t = lane_value(vt, bit);
-                        j1n = lane_value(vn, bit);
-                    } else if (found == 1) {
-                        j2 = r0 + bit;
-                    }
+                const bool hit = r < nrows && (s_sub[r * 20 + ia] == idA || s_sub[r * 20 + ib] == idB);
+                unsigned long long b = __ballot(hit);
+                while (b && found < 3) {
+                    const int bit = __ffsll((long long)b) - 1;
+                    b &= b - 1;
+                    if (found == 0) j1 = r0 + bit;
+                    else if (found == 1) j2 = r0 + bit;
                     ++found;
                 }
             }
@@ -1028,9 +1000,12 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
                 status = -6;
                 break;
             }
-            bool add_b = false;  // row j1 takes part B (found == 1 when it holds another B; found == 2 not disjoint)
             if (found == 1) {
-                add_b = j1b != idB;
+                if (lane == 0 && s_sub[j1 * 20 + ib] != idB) {
+                    s_sub[j1 * 20 + ib] = idB;
+                    s_sub[j1 * 20 + 19] = s_sub[j1 * 20 + 19] + 1.0;
+                    s_sub[j1 * 20 + 18] = s_sub[j1 * 20 + 18] + (s_sb[c] + s);
+                }
             } else if (found == 2) {
                 const bool both = lane < 18 && s_sub[j1 * 20 + lane] >= 0.0 && s_sub[j2 * 20 + lane] >= 0.0;
                 if (__ballot(both) == 0ull) {  // disjoint: merge j2 into j1, drop j2
@@ -1039,27 +1014,17 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
                     __syncthreads();
                     if (lane == 0) s_sub[j1 * 20 + 18] = s_sub[j1 * 20 + 18] + s;
                     __syncthreads();
-                    // rows j2 + 1 .. nrows - 1 move up one row: 4 values per lane per round, all
-                    // read before any is written (a round's targets end before its sources)
-                    const int first = j2 * 20, nmove = (nrows - 1 - j2) * 20;
-                    for (int e0 = 0; e0 < nmove; e0 += 256) {
-                        double v[4];
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const int e = e0 + t * 64 + lane;
-                            v[t] = e < nmove ? s_sub[first + 20 + e] : 0.0;
-                        }
+                    for (int r = j2; r < nrows - 1; ++r) {
+                        double v = lane < 20 ? s_sub[(r + 1) * 20 + lane] : 0.0;
                         __syncthreads();
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const int e = e0 + t * 64 + lane;
-                            if (e < nmove) s_sub[first + e] = v[t];
-                        }
+                        if (lane < 20) s_sub[r * 20 + lane] = v;
                         __syncthreads();
                     }
                     --nrows;
-                } else {
-                    add_b = true;
+                } else if (lane == 0) {
+                    s_sub[j1 * 20 + ib] = idB;
+                    s_sub[j1 * 20 + 19] = s_sub[j1 * 20 + 19] + 1.0;
+                    s_sub[j1 * 20 + 18] = s_sub[j1 * 20 + 18] + (s_sb[c] + s);
                 }
             } else if (k < 17) {
                 if (nrows >= maxp) {
@@ -1071,15 +1036,10 @@ __global__ __launch_bounds__(64) void assemble_people(const Conn* __restrict__ c
                     if (lane == ia) v = idA;
                     if (lane == ib) v = idB;
                     if (lane == 19) v = 2.0;
-                    if (lane == 18) v = (sa + sb) + s;
+                    if (lane == 18) v = (s_sa[c] + s_sb[c]) + s;
                     s_sub[nrows * 20 + lane] = v;
                 }
                 ++nrows;
-            }
-            if (add_b && lane == 0) {
-                s_sub[j1 * 20 + ib] = idB;
-                s_sub[j1 * 20 + 19] = j1n + 1.0;
-                s_sub[j1 * 20 + 18] = j1t + (sb + s);
             }
             __syncthreads();
         }
