@@ -13,6 +13,6 @@ for L in pytorch-openpose_amd/lib/ab_base.so ""; do
   python -c "
 import json; d = json.loads(open('gpurun_out/ab_bench.json').read().strip().splitlines()[-1])
 s = d['stage_ms_per_step']
-print('lib %s: %.1f frames/s  C2 %.3f ms  hand %.3f ms  serial 3x3 %.4f 7x7 %.4f 1x1 %.4f assemble %.4f | pipelined assemble %.4f' % ('base' if '$L' else 'new', d['value'], d['latency_ms_single_frame'], d['c3_hand']['latency_ms'], s['conv3x3'], s['conv7x7'], s['conv1x1'], s['assemble'], d['stage_ms_per_step_pipelined']['assemble']))"
+print('lib %s: %.1f frames/s  C2 %.3f ms  hand %.3f ms  serial 3x3 %.4f 7x7 %.4f 1x1 %.4f assemble %.4f gauss %.4f | pipelined assemble %.4f gauss %.4f' % ('base' if '$L' else 'new', d['value'], d['latency_ms_single_frame'], d['c3_hand']['latency_ms'], s['conv3x3'], s['conv7x7'], s['conv1x1'], s['assemble'], s['gauss_nms_resize'], d['stage_ms_per_step_pipelined']['assemble'], d['stage_ms_per_step_pipelined']['gauss_nms_resize']))"
 done
 done
