@@ -212,6 +212,35 @@ def test_destroyed_handles_graphs_do_not_break_replays():
             same("one", hs["one"](img))
 
 
+def test_alternating_shapes_on_one_handle():
+    """One Body and one Hand fed frames of alternating sizes, each size three times in a row
+    (eager, capture, replay) and then again after other sizes: the larger sizes grow the workspace,
+    which invalidates every captured graph (g_alloc_epoch), and the per-signature launch plans and
+    slab schedules pile up.  Every call equals an eager (OPOSE_NO_GRAPH=1) handle's call on the
+    same frame, bit for bit."""
+    from src.body import Body
+    from src.hand import Hand
+    from src.weights import seeded_state_dict
+    rng = np.random.default_rng(27)
+    frames = [rng.integers(0, 256, s, dtype=np.uint8) for s in ((96, 128, 3), (184, 232, 3), (368, 656, 3))]
+    crops = [rng.integers(0, 256, (s, s, 3), dtype=np.uint8) for s in (128, 256, 184)]
+    bsd, hsd = seeded_state_dict("body", 0), seeded_state_dict("hand", 0)
+    os.environ["OPOSE_NO_GRAPH"] = "1"
+    try:
+        eb, eh = Body(bsd), Hand(hsd)
+    finally:
+        del os.environ["OPOSE_NO_GRAPH"]
+    ref_b = [eb(f) for f in frames]
+    ref_h = [eh(c) for c in crops]
+    gb, gh = Body(bsd), Hand(hsd)
+    for i in (0, 1, 0, 2, 1, 0, 2):
+        for _ in range(3):
+            cand, sub = gb(frames[i])
+            assert np.array_equal(cand, ref_b[i][0]) and np.array_equal(sub, ref_b[i][1]), i
+            pk = gh(crops[i])
+            assert pk.dtype == ref_h[i].dtype and np.array_equal(pk, ref_h[i]), i
+
+
 def test_forward_waits_for_half_input(body):
     x = torch.from_numpy(np.random.default_rng(6).standard_normal((1, 3, 64, 96)).astype(np.float32))
     xh = x.half()
