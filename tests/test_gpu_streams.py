@@ -241,6 +241,49 @@ def test_alternating_shapes_on_one_handle():
             assert pk.dtype == ref_h[i].dtype and np.array_equal(pk, ref_h[i]), i
 
 
+def test_handles_on_concurrent_threads():
+    """Serving threads with a handle each (ctypes drops the GIL, so the library calls overlap):
+    a Body and a Hand thread plus a second Body thread on other frames, 6 calls each (eager,
+    capture, replays: the captures are thread-local, the workspace epoch and the scale-stream pool
+    are process-wide), all equal to the same handles' single-threaded results."""
+    import threading
+    from src.body import Body
+    from src.hand import Hand
+    from src.weights import seeded_state_dict
+    rng = np.random.default_rng(29)
+    img_a = rng.integers(0, 256, (184, 232, 3), dtype=np.uint8)
+    img_b = rng.integers(0, 256, (96, 176, 3), dtype=np.uint8)
+    crop = rng.integers(0, 256, (128, 128, 3), dtype=np.uint8)
+    bsd, hsd = seeded_state_dict("body", 0), seeded_state_dict("hand", 0)
+    jobs = {"body_a": (Body(bsd, scale_search=(0.5, 1.0)), img_a), "body_b": (Body(bsd), img_b),
+            "hand": (Hand(hsd), crop)}
+    ref = {k: h(x) for k, (h, x) in jobs.items()}
+    outs = {k: [] for k in jobs}
+    errors = []
+
+    def run(k):
+        h, x = jobs[k]
+        try:
+            for _ in range(6):
+                outs[k].append(h(x))
+        except Exception as e:  # reported in the main thread
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in jobs]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts) and not errors, errors
+    for k, res in outs.items():
+        assert len(res) == 6, k
+        for out in res:
+            if k == "hand":
+                assert np.array_equal(out, ref[k]), k
+            else:
+                assert np.array_equal(out[0], ref[k][0]) and np.array_equal(out[1], ref[k][1]), k
+
+
 def test_forward_waits_for_half_input(body):
     x = torch.from_numpy(np.random.default_rng(6).standard_normal((1, 3, 64, 96)).astype(np.float32))
     xh = x.half()
