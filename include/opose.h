@@ -93,6 +93,7 @@ typedef struct opose_params {
 void opose_default_params(int net, opose_params* p);
 
 /* ---- lifetime ---------------------------------------------------------------------- */
+/* A handle is used by one thread at a time; handles on different threads run concurrently. */
 int opose_create(int device, opose_t** out);
 void opose_destroy(opose_t* h);
 const char* opose_last_error(const opose_t* h);
