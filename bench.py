@@ -263,36 +263,114 @@ def max_over_ranks(x, dev):
     return float(t.item())
 
 
-def host_to_host(body, frames_np, steps, dev, rank, world):
+def numa_info(ptr, dev):
+    """NUMA node of the pinned host buffer at `ptr` (/proc/self/numa_maps) and of the GPU's PCI
+    device, so that a box-dependent PCIe rate can be attributed."""
+    out = {"buffer_numa": None, "gpu_numa": None}
+    try:
+        for line in open("/proc/self/numa_maps"):
+            addr, rest = line.split(" ", 1)
+            # numa_maps lists VMAs by start address only: take the last VMA starting at or below ptr
+            if int(addr, 16) <= ptr:
+                nodes = {k[1:]: int(v) for k, v in (f.split("=") for f in rest.split() if f[:1] == "N" and "=" in f)}
+                out["buffer_numa"] = nodes or None
+    except (OSError, ValueError):
+        pass
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bus = "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        out["gpu_pci"] = bus
+        out["gpu_numa"] = int(open(f"/sys/bus/pci/devices/{bus}/numa_node").read())
+    except (OSError, ValueError, AttributeError, TypeError):
+        pass
+    return out
+
+
+def copy_rates(host, dbuf, rhost, rdev, reps=5):
+    """Standalone pinned-copy rates of the host-to-host pass's own buffers (GB/s, event-timed on
+    an otherwise idle stream): what one step's upload and download cost on this box's link."""
+    st = torch.cuda.Stream(device=dbuf.device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    res = {}
+    for name, dst, src in (("h2d", dbuf, host), ("d2h", rhost, rdev)):
+        with torch.cuda.stream(st):
+            dst.copy_(src, non_blocking=True)
+            e0.record(st)
+            for _ in range(reps):
+                dst.copy_(src, non_blocking=True)
+            e1.record(st)
+        e1.synchronize()
+        res[name + "_GBps"] = round(reps * src.numel() * src.element_size() / (e0.elapsed_time(e1) * 1e-3) / 1e9, 2)
+    return res
+
+
+def host_to_host(body, frames_np, steps, dev, rank, world, mode=None):
     """PCIe-inclusive rate (the reference's boundary, src/body.py:44-50): pinned host frames
-    uploaded each step on a copy stream per frame buffer (double-buffered, overlapped with the
-    previous step's compute), records downloaded to pinned host memory each step."""
+    uploaded every step, records downloaded to pinned host memory every step.
+
+    Each cross-stream wait stands for exactly one data dependency (round 6; round 5's pass had
+    each upload wait for the whole previous step's post-processing and queued the download on
+    the post stream, 8-11 % below the device-resident rate on the driver's boxes):
+    * the upload of step k+2's frames into dbuf[k%2] runs on cps[k%2] once step k's network has
+      read that buffer (Handle.signal_input -> opose_signal_input: an event behind the network
+      part on its own stream, not behind the post-network kernels on the handle's stream);
+    * mode "sync" (default with the pipelined overlap): the host waits for the upload's own
+      event, then makes the call with wait=False (OPOSE_PIPELINE's contract: the frames are
+      complete when the call is made), so no marker is recorded on a caller stream at call time.
+      Streams beyond the box's hardware queues share them, and a marker queued behind the
+      handle's post-processing in a shared queue held the next network back (scripts/h2h_ab.py,
+      profiles/r6_h2h_*); mode "stream": the call is made on cps[k%2] (opose_wait_stream);
+    * step k's records go down on a stream of their own after an event behind its post-processing
+      (and the RCCL gather), so step k+1's post is not queued behind the copy; the handle's stream
+      waits for that download before step k+2 rewrites rdev[k%2]."""
+    mode = mode or ("sync" if PIPELINE else "stream")
     B = len(frames_np)
     host = torch.from_numpy(frames_np).pin_memory()
     rb = body.handle.record_bytes()
     dbuf = [torch.empty_like(host, device=dev) for _ in range(2)]
     rdev = [torch.empty((B, rb), dtype=torch.uint8, device=dev) for _ in range(2)]
-    rhost = [torch.empty((B, rb), dtype=torch.uint8).pin_memory() for _ in range(2)]
+    rhost = [torch.empty((world * B if world > 1 else B, rb), dtype=torch.uint8).pin_memory() for _ in range(2)]
     cps = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    dls = torch.cuda.Stream(device=dev)
+    posted = [torch.cuda.Event() for _ in range(2)]
+    uploaded = [torch.cuda.Event() for _ in range(2)]
+    landed = [torch.cuda.Event() for _ in range(2)]
     lib_stream = body.handle.torch_stream()
     from src.dist import gather_records
+    info = dict(numa_info(host.data_ptr(), dev), **copy_rates(host, dbuf[0], rhost[0][:B], rdev[0]))
+    info["upload_bytes_per_step"] = host.numel()
+    info["download_bytes_per_step"] = rhost[0].numel() if rank == 0 else 0
+    info["mode"] = mode
 
     def upload(i):
-        cps[i].wait_stream(lib_stream)  # the call that last read dbuf[i] has finished with it
+        body.handle.signal_input(cps[i])  # the network that last read dbuf[i] is done with it
         with torch.cuda.stream(cps[i]):
             dbuf[i].copy_(host, non_blocking=True)
+            uploaded[i].record(cps[i])
 
     def run(n):
         for i in range(2):
             upload(i)
         for k in range(n):
             i = k % 2
-            with torch.cuda.stream(cps[i]):  # the library waits for this buffer's upload only
-                body.infer_records(dbuf[i], rdev[i], pipeline=PIPELINE)
+            if k >= 2:
+                lib_stream.wait_event(landed[i])  # step k-2's download has read rdev[i]
+            if mode == "sync":
+                uploaded[i].synchronize()
+                body.infer_records(dbuf[i], rdev[i], pipeline=True, wait=False)
+            else:
+                with torch.cuda.stream(cps[i]):  # the library waits for this buffer's upload only
+                    body.infer_records(dbuf[i], rdev[i], pipeline=PIPELINE)
             with torch.cuda.stream(lib_stream):
                 allrec = gather_records(rdev[i], world * B, world) if world > 1 else rdev[i]
-                if rank == 0:
-                    rhost[i].copy_(allrec[:B] if world > 1 else allrec, non_blocking=True)
+                posted[i].record(lib_stream)
+            if rank == 0:
+                dls.wait_event(posted[i])
+                with torch.cuda.stream(dls):
+                    rhost[i].copy_(allrec, non_blocking=True)
+                if world > 1:
+                    allrec.record_stream(dls)
+            landed[i].record(dls)
             if k + 2 < n:
                 upload(i)
         body.handle.synchronize()
@@ -309,7 +387,7 @@ def host_to_host(body, frames_np, steps, dev, rank, world):
     dt = time.perf_counter() - t0
     if world > 1:
         dt = max_over_ranks(dt, dev)
-    return world * B * steps / dt, dt / steps * 1e3
+    return world * B * steps / dt, dt / steps * 1e3, info
 
 
 def hand_c3(device, iters):
@@ -460,7 +538,7 @@ def main():
         if prof_pipe:
             prof_pipe = {k: v for k, v in prof_pipe.items() if not k.startswith("layer/")}
     # host-to-host (PCIe-inclusive) pass: reported beside `value`, never as it
-    h2h_value, h2h_ms = host_to_host(body, frames_np, args.host_steps or args.steps, dev, rank, world)
+    h2h_value, h2h_ms, h2h_info = host_to_host(body, frames_np, args.host_steps or args.steps, dev, rank, world)
 
     c3 = hand_c3(local, args.latency_iters) if rank == 0 and args.latency_iters > 0 else None
 
@@ -507,10 +585,12 @@ def main():
                        if PIPELINE else "none"},
             "frames_total": frames_total,
             "value_host_to_host": h2h_value,
-            "host_to_host": {"ms_per_step": h2h_ms, "basis": "pinned host frames uploaded each step on per-buffer "
-                             "copy streams (double-buffered, overlapped), records (and the RCCL gather when "
-                             "n_gpus > 1) downloaded to pinned host memory each step; reference boundary "
-                             "src/body.py:44-50"},
+            "value_host_to_host_ratio": h2h_value / (frames_total / dt),
+            "host_to_host": dict(h2h_info, ms_per_step=h2h_ms, basis=(
+                "pinned host frames uploaded each step on per-buffer copy streams once the previous "
+                "network has read the buffer (opose_signal_input), records (and the RCCL gather when "
+                "n_gpus > 1) downloaded to pinned host memory each step on a stream of their own; "
+                "reference boundary src/body.py:44-50")),
             "roofline": {"bound": "mfma", "kernel": CONV_KERNEL + " (7x7 CPM stages)",
                          "achieved": achieved, "peak": PEAK_CONV_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_CONV_TFLOPS,

@@ -116,6 +116,14 @@ int opose_flush(opose_t* h);
  *                        the handle read can be freed or reused by `hip_stream`. */
 int opose_wait_stream(opose_t* h, void* hip_stream);
 int opose_signal_stream(opose_t* h, void* hip_stream);
+/*   opose_signal_input:  work queued on `hip_stream` from now on starts once the handle has read
+ *                        the device inputs of every call made so far, so those buffers may be
+ *                        refilled there.  After OPOSE_PIPELINE calls that is the end of the last
+ *                        call's network part, before its post-network part: the next frames'
+ *                        upload overlaps the post-network kernels instead of waiting for them
+ *                        (the reference's per-frame `.cuda()` upload, src/body.py:44-45, in a
+ *                        video loop).  Otherwise it is opose_signal_stream. */
+int opose_signal_input(opose_t* h, void* hip_stream);
 
 /* Capacity of one Body record: peaks kept per part and people kept per frame.
  * Defaults 96 / 96.  Overflow makes the frame's status OPOSE_E_CAPACITY. */

@@ -384,6 +384,7 @@ struct opose_ctx {
     // opose_wait_stream / opose_signal_stream / opose_set_stream: ordering against streams the
     // caller owns (a framework's current stream)
     hipEvent_t ev_ext = nullptr, ev_sig = nullptr;
+    hipEvent_t ev_in = nullptr;  // opose_signal_input
     bool post_pending[2] = {false, false};
     bool main_dirty = false;
     int mid_set = 0, next_set = 0;
@@ -459,7 +460,7 @@ struct opose_ctx {
             if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
         graphs.clear();
         return_stream(nstream, device, nstream_prio);
-        for (hipEvent_t e : {ev_net, ev_main, ev_post[0], ev_post[1], ev_ext, ev_sig, ev_fork})
+        for (hipEvent_t e : {ev_net, ev_main, ev_post[0], ev_post[1], ev_ext, ev_sig, ev_in, ev_fork})
             if (e) (void)hipEventDestroy(e);
         for (int i = 0; i < kMaxScales; ++i) {
             return_stream(sstream[i], device, 0);
@@ -2372,6 +2373,25 @@ int opose_signal_stream(opose_t* h, void* s) {
         if (xs == h->stream) return OPOSE_OK;
         hipEvent_t e = lazy_event(h->ev_sig);
         OPOSE_HIP_CHECK(hipEventRecord(e, h->stream));
+        OPOSE_HIP_CHECK(hipStreamWaitEvent(xs, e, 0));
+    });
+    return OPOSE_OK;
+}
+
+int opose_signal_input(opose_t* h, void* s) {
+    if (!h) return OPOSE_E_ARG;
+    // Since the last entry point that queued work on the handle's stream (main_dirty), only
+    // OPOSE_PIPELINE calls ran, and each read its device inputs on the network stream only (its
+    // post-network part reads the mid buffers).  That stream waited for the handle's stream when
+    // main_dirty was last cleared, so an event on it after the last network covers every input
+    // read so far.  Otherwise the handle's stream holds input reads: opose_signal_stream.
+    if (!h->nstream || h->main_dirty) return opose_signal_stream(h, s);
+    OPOSE_TRY(h, {
+        OPOSE_HIP_CHECK(hipSetDevice(h->device));
+        const hipStream_t xs = static_cast<hipStream_t>(s);
+        if (xs == h->nstream) return OPOSE_OK;
+        hipEvent_t e = lazy_event(h->ev_in);
+        OPOSE_HIP_CHECK(hipEventRecord(e, h->nstream));
         OPOSE_HIP_CHECK(hipStreamWaitEvent(xs, e, 0));
     });
     return OPOSE_OK;

@@ -45,6 +45,7 @@ def _load():
         "opose_set_stream": (I, [P, P]),
         "opose_wait_stream": (I, [P, P]),
         "opose_signal_stream": (I, [P, P]),
+        "opose_signal_input": (I, [P, P]),
         "opose_get_stream": (P, [P]),
         "opose_synchronize": (I, [P]),
         "opose_flush": (I, [P]),
@@ -97,7 +98,7 @@ def _load():
 lib = _load()
 
 EXPORTED = ["opose_default_params", "opose_create", "opose_destroy", "opose_last_error", "opose_set_stream",
-            "opose_wait_stream", "opose_signal_stream",
+            "opose_wait_stream", "opose_signal_stream", "opose_signal_input",
             "opose_get_stream", "opose_synchronize", "opose_flush", "opose_set_capacity", "opose_body_record_bytes",
             "opose_load_weights", "opose_body_forward", "opose_hand_forward", "opose_hand_forward_pyramid",
             "opose_body_infer",
@@ -249,6 +250,15 @@ class Handle:
         """Torch's current stream continues after everything queued on the handle: outputs are
         complete for torch consumers and the inputs the handle read may be freed/reused."""
         self.check(lib.opose_signal_stream(self.h, self._torch_stream()))
+
+    def signal_input(self, stream=None):
+        """Work queued on `stream` (a torch.cuda.Stream; default torch's current stream) from now on
+        starts once the handle has read the device inputs of every call so far: after pipelined
+        calls, the end of the last call's network part (opose_signal_input)."""
+        import torch
+        self._adopt_torch_stream()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.check(lib.opose_signal_input(self.h, C.c_void_p(st.cuda_stream or None)))
 
     def hold(self, *tensors):
         """Keep the caching allocator from reusing these tensors' memory until the handle's

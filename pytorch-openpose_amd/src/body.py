@@ -231,7 +231,7 @@ class Body(object):
             return [self._decode(r) for r in rec]
 
     # ------------------------------------------------------------------ device API
-    def infer_records(self, frames_dev, records_dev=None, pipeline=False):
+    def infer_records(self, frames_dev, records_dev=None, pipeline=False, wait=True):
         """frames_dev: torch.uint8 cuda [N,H,W,3]; returns a torch.uint8 cuda [N, record_bytes] tensor.
 
         Asynchronous (no host synchronisation): ordered after torch's current stream, and the
@@ -242,7 +242,12 @@ class Body(object):
         call's post-processing (video-batch throughput).  pipeline="defer"
         (OPOSE_PIPELINE_DEFER): this call's post-processing is enqueued by the next pipelined
         call once that call's network reaches conv3_1, or by handle.flush() / synchronize() /
-        decode_records(); keep frames and records alive until then."""
+        decode_records(); keep frames and records alive until then.
+        wait=False (pipelined calls only): do not order the call after torch's current stream.
+        The caller guarantees that the frames are complete and that the records buffer is free
+        (e.g. it synchronized the host on the upload's event): opose_wait_stream would put a
+        marker on the caller's stream, and a stream that shares a hardware queue with the
+        handle's post-processing stream then holds the next network back behind that work."""
         import torch
         N, H, W, _ = frames_dev.shape
         if frames_dev.stride(3) != 1 or frames_dev.stride(2) != 3:
@@ -253,7 +258,8 @@ class Body(object):
         rb = self.handle.record_bytes()
         if records_dev is None:
             records_dev = torch.empty((N, rb), dtype=torch.uint8, device=frames_dev.device)
-        self.handle.wait_torch()  # frames / records produced or last used on torch's stream
+        if wait or not pipeline:
+            self.handle.wait_torch()  # frames / records produced or last used on torch's stream
         rc = _native.lib.opose_body_infer(self.handle.h, frames_dev.data_ptr(), N, H, W, row_stride,
                                           frame_stride, self.params, records_dev.data_ptr(),
                                           _native.IN_DEVICE | _native.OUT_DEVICE
