@@ -95,6 +95,8 @@ struct X6Group {
     // of the layer and the segment's logical geometry only (engine.cpp slab_count), never of the
     // launch's grid, groups or row band: a pixel sums in the same order whatever launch computes it.
     int slabs;
+    int tpf;               // conv_wino_x6: tile slots per frame (frame-aligned blocks of 128), 0: tiles
+                           // numbered across frames (set by the launcher; npix = tile slots)
     int t0;                // first tile of the group in the launch's tile space (set by the launcher)
     int u0;                // first work unit (tile, slab) of the group (set by the launcher)
 };

@@ -88,6 +88,11 @@ bool conv_win_fits(int N, int H, int W, int ks);
 // the window of any 256-pixel run of one frame W columns wide fits the LDS (whatever the height)
 bool conv_win_fits_rows(int W, int ks);
 void launch_conv_win_x6(const X6Args& a, hipStream_t st);
+// Winograd F(2,3) along x for 3x3 layers on X6P inputs (conv_wino.hip): weights U_v in pair order,
+// tile slots per frame of a batch (-1: the window does not fit), whole-tile launch
+void x6_pack_weights_wino(const float* w, int cout, int cin, int Mpad, int* nK_out, std::vector<uint16_t>& out);
+int wino_tpf(int N, int H, int W);
+void launch_conv_wino_x6(const X6Args& a, hipStream_t st);
 // imgproc.hip
 void launch_preprocess(const uint8_t* src, int64_t frame_stride, int64_t row_stride, int N, int H, int W, int Hs,
                        int Ws, double sy, double sx, int Hp, int Wp, float pad_val, float* out, hipStream_t st);

@@ -23,6 +23,22 @@ def golden_image(d):
     return img
 
 
+# lines a passing test wants in the run's log (pytest captures their prints): written in the
+# terminal summary, e.g. the moved-keypoint count of every end-to-end fixture
+REPORT_LINES = []
+
+
+def report(line: str):
+    REPORT_LINES.append(line)
+
+
+def pytest_terminal_summary(terminalreporter):
+    if REPORT_LINES:
+        terminalreporter.section("libopose parity report")
+        for line in REPORT_LINES:
+            terminalreporter.write_line(line)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libopose.so on cuda:0)")
     config.addinivalue_line("markers", "slow: long-running CPU test")

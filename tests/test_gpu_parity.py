@@ -15,7 +15,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import GOLDEN, golden_image
+from conftest import GOLDEN, golden_image, report
 
 pytestmark = pytest.mark.gpu
 
@@ -200,11 +200,12 @@ def test_network_full_size_and_batch_vs_oracle():
 
 
 # Keypoints the GPU may place on the other pixel of a float64 plateau (oracle/ties.py: smoothed
-# values within 1e-6 of the part map's max), per fixture -- the counts observed on hardware (round 5), never
-# more than the reference moves against itself at that size (profiles/r5_ref_thread_noise.json:
-# body_e2e_31 at 1 / 16 torch threads moves 4 / 2 of its own 1,350 keypoints, all onto such
-# plateaus; on body_e2e_21 / 22 it moves none).  Every other fixture: exact pixels.
-_TIE_ALLOWANCE = {"body_e2e_21_96x128.npz": 1, "body_e2e_31_368x656.npz": 3}
+# values within 1e-6 of the part map's max), per fixture -- the count observed on hardware (rounds
+# 5 and 6: 3 of 1,350), within what the reference moves against itself at that size
+# (profiles/r5_ref_thread_noise.json: body_e2e_31 at 1 / 16 torch threads moves 4 / 2 of its own
+# keypoints, all onto such plateaus).  Every other fixture, body_e2e_21 / 22 included (the
+# reference never tips them, and the library's summation order is fixed per layer): exact pixels.
+_TIE_ALLOWANCE = {"body_e2e_31_368x656.npz": 3}
 
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "body_e2e_*.npz"))), ids=os.path.basename)
@@ -213,8 +214,8 @@ def test_body_end_to_end_vs_reference(body, path):
     src/body.py Body.__call__ on src/model.py's network, 8 torch threads): the north-star bar,
     identical keypoint pixels and identical person/subset assignment -- except on fixtures listed in
     _TIE_ALLOWANCE, where at most that many keypoints may sit one pixel from the reference's on a
-    float64 plateau of the smoothed heat map (body_e2e_21: one, 2e-7 apart; the fp32 summation
-    order decides it, as the reference's own thread count does at C2's size).  Such keypoints' ids
+    float64 plateau of the smoothed heat map (body_e2e_31: three of 1,350; the fp32 summation order
+    decides them, as the reference's own thread count does at C2's size).  Such keypoints' ids
     are mapped; the people and their assignment must still be identical, and only the scores of
     the people holding a moved keypoint may change beyond rtol 1e-3 (to 3e-2: the keypoint's heat
     value and its limbs' PAF integrals move with it)."""
@@ -228,7 +229,10 @@ def test_body_end_to_end_vs_reference(body, path):
     ids = np.arange(len(cand), dtype=np.float64)
     moved = []  # reference ids of keypoints on another (tied) pixel
     allowance = _TIE_ALLOWANCE.get(os.path.basename(path), 0)
-    if not np.array_equal(cand[:, :2], ref_c[:, :2]):
+    same = np.array_equal(cand[:, :2], ref_c[:, :2])
+    if same:  # the driver's log shows the count for every fixture, zero included
+        report(f"{os.path.basename(path)}: 0 of {len(ref_c)} keypoints across float64 plateaus (allowed {allowance})")
+    if not same:
         assert allowance, "keypoint pixels differ on a fixture with no tie allowance"
         up, blur = ties.f64_smoothed(img, oracle_sd("body", 0))
         pairs = ties.tie_pairs(up, blur, cand, ref_c)
@@ -237,7 +241,8 @@ def test_body_end_to_end_vs_reference(body, path):
             ids[i] = j
             if not np.array_equal(cand[i, :2], ref_c[j, :2]):
                 moved.append(j)
-        print(f"{os.path.basename(path)}: {len(moved)} keypoint(s) across float64 plateaus (allowed {allowance})")
+        report(f"{os.path.basename(path)}: {len(moved)} of {len(ref_c)} keypoints across float64 plateaus "
+               f"(allowed {allowance})")
         assert len(moved) <= allowance, (len(moved), allowance)
         keep = np.setdiff1d(np.arange(len(cand)), list(pairs))
         assert np.array_equal(cand[keep, :2], ref_c[keep, :2])

@@ -189,3 +189,56 @@ def test_body_1080p_full_network_equals_scale_decomposition():
     assert cand.ndim == 2 and cand.shape[1] == 4 and subset.shape[1] == 20
     maps = [body.scale_maps(img[None], s) for s in range(len(SCALES))]
     _identical(body.post_scales(maps, 1080, 1920), whole)
+
+
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("scales", [(0.5, 1.0), (1.0, 1.5, 2.0), SCALES], ids=["2scales", "3scales", "4scales"])
+def test_heat_full_scales_equals_per_scale_launches(scales):
+    """The one-launch multi-scale heat average (imgproc.hip heat_full_scales, default) against one
+    launch per scale into the float64 accumulator (OPOSE_HEAT_SCALES=0, read at handle creation):
+    every scale's resize summed in scale order from 0.0 either way, so the records are identical
+    bit for bit.  Two planted 368 x 656 frames per call (N = 2); at 368 rows the 1.0 scale is
+    identity-sized (x8 of the 46-row map is the frame)."""
+    from oracle.body_post import preprocess
+    from src.body import Body
+    from src.weights import seeded_state_dict
+    H, W = 368, 656
+    lowres = [_pyramid(H, W, n, seed) for n, seed in ((5, 41), (2, 42))]
+    idx = [SCALES.index(s) for s in scales]
+    maps = [np.concatenate([np.concatenate([lr[i][0], lr[i][1]], 0)[None] for lr in lowres], 0) for i in idx]
+    for k, s in enumerate(scales):
+        _, _, padded = preprocess(np.zeros((H, W, 3), np.uint8), s * 368 / H)
+        assert maps[k].shape[2:] == (padded[0] // 8, padded[1] // 8)
+    outs = []
+    for on in ("1", "0"):
+        b = _with_env({"OPOSE_HEAT_SCALES": on}, lambda: Body(seeded_state_dict("body", 0), scale_search=scales))
+        outs.append(b.post_scales(maps, H, W))
+        del b
+    assert len(outs[0]) == 2
+    _identical(outs[0], outs[1])
+    assert any(len(sub) for _, sub in outs[0])
+
+
+def test_hand_heat_full_scales_equals_per_scale_launches():
+    """The same for Hand(): its four scales' heat average in one launch (default) or per scale."""
+    from src.hand import Hand
+    from src.weights import seeded_state_dict
+    crop = np.random.default_rng(43).integers(0, 256, (200, 200, 3), dtype=np.uint8)
+    outs = []
+    for on in ("1", "0"):
+        hd = _with_env({"OPOSE_HEAT_SCALES": on}, lambda: Hand(seeded_state_dict("hand", 0)))
+        outs.append(hd(crop))
+        del hd
+    assert outs[0].dtype == outs[1].dtype and np.array_equal(outs[0], outs[1])

@@ -74,6 +74,59 @@ def test_x6_conv_fp32_accuracy(native, handle, N, Cin, H, W, Cout, ks, mt, pt, s
     assert np.array_equal(y6, y6x)  # split epilogue + rebuild is lossless
 
 
+WINO_CASES = [
+    (2, 128, 23, 41, 256),   # H/8 of the bench: odd W, tile blocks across frames
+    (2, 256, 46, 82, 128),   # H/4: windows across frames too long -> frame-aligned tile blocks
+    (1, 64, 17, 30, 128),    # one frame, even W, 6 chunks (two four-group periods)
+    (3, 40, 11, 13, 128),    # 5 channel groups: 15 pairs, the last chunk padded
+    (1, 512, 23, 41, 512),   # conv4_2 on one frame
+    (2, 128, 9, 7, 96),      # Cout < 128 (Mpad 128), W = 7
+]
+
+
+@pytest.mark.parametrize("N,Cin,H,W,Cout", WINO_CASES)
+def test_wino_conv_fp32_accuracy(native, handle, N, Cin, H, W, Cout):
+    """conv_wino_x6 (Winograd F(2,3) along x, csrc/conv_wino.hip) on padded X6P inputs through the
+    engine's launch path (opose_debug_conv_x6 with mt = -3 forces the family) against a float64
+    reference: the same bar as the direct kernels -- |err| <= 4e-6 * conv(|x|, |w|) + 1e-6 and
+    the mean relative error within 3x the fp32 MFMA kernel's.  The window kernel on the same
+    padded inputs (mt = -2) is checked to the same bar beside it."""
+    rng = np.random.default_rng(Cin * 3 + W)
+    x = np.maximum(rng.standard_normal((N, Cin, H, W), dtype=np.float32), 0)
+    w = rng.standard_normal((Cout, Cin, 3, 3), dtype=np.float32) * np.float32(np.sqrt(2 / (Cin * 9)))
+    b = rng.standard_normal(Cout, dtype=np.float32) * np.float32(0.1)
+    yw = _run(native, handle, native.lib.opose_debug_conv_x6, x, w, b, True, -3, 0, 0, 1)
+    yd = _run(native, handle, native.lib.opose_debug_conv_x6, x, w, b, True, -2, 0, 0, 1)
+    y32 = _run(native, handle, native.lib.opose_debug_conv, x, w, b, True, 0, 0, 0)
+    xd, wd, bd = (torch.from_numpy(a).double() for a in (x, w, b))
+    ref = F.conv2d(xd, wd, bd, padding=1).clamp_min(0).numpy()
+    mag = F.conv2d(xd.abs(), wd.abs(), bd.abs(), padding=1).numpy()
+    e32 = (np.abs(y32 - ref) / np.maximum(mag, 1e-30)).mean()
+    for y in (yw, yd):
+        e = np.abs(y - ref)
+        assert (e <= 4e-6 * mag + 1e-6).all(), float((e / (4e-6 * mag + 1e-6)).max())
+        assert (e / np.maximum(mag, 1e-30)).mean() <= 3 * e32 + 1e-9
+    print(f"wino mean rel err {(np.abs(yw - ref) / np.maximum(mag, 1e-30)).mean():.3e}, "
+          f"window {(np.abs(yd - ref) / np.maximum(mag, 1e-30)).mean():.3e}, fp32 {e32:.3e}")
+
+
+@pytest.mark.parametrize("kind,shape", [("body", (4, 3, 184, 328)), ("body", (1, 3, 368, 656)),
+                                        ("hand", (1, 3, 368, 368))], ids=["body4x184x328", "body368x656", "hand368"])
+def test_network_wino_vs_window(native, kind, shape):
+    """The network with its 3x3 layers on conv_wino_x6 (OPOSE_WINO=1, opt-in) against the default
+    window kernel: a different summation order, so the bar is the network tolerance and a maximum
+    deviation below 1e-5 of the map's range."""
+    from src.model import bodypose_model, handpose_model
+    cls = bodypose_model if kind == "body" else handpose_model
+    x = np.random.default_rng(12).random(shape, dtype=np.float32) - np.float32(0.5)
+    on = _model_outputs(cls, kind, x, {"OPOSE_WINO": "1"})
+    off = _model_outputs(cls, kind, x, {"OPOSE_WINO": "0"})
+    for a, r in zip(on, off):
+        tol = 2e-4 * np.abs(r).max() + 2e-4 * np.abs(r)
+        assert (np.abs(a - r) <= tol).all(), kind
+        assert np.abs(a - r).max() <= 1e-5 * np.abs(r).max(), kind
+
+
 def test_x6_split_roundtrip_exact(native, handle):
     """A 1x1 identity conv through the X6 epilogue reproduces every fp32 input bit-exactly
     (subnormal-free, both signs, magnitudes over 2^-60 .. 2^60)."""
