@@ -417,8 +417,9 @@ def hand_c3(device, iters):
     return {"workload": "C3 Hand(): one 368x368 crop, scale_search [0.5, 1, 1.5, 2], host in -> host out",
             "latency_ms": ms, "conv_tflop_per_call": flops / 1e12,
             "conv_ms_per_call": conv_ms,
-            # the four scales' networks run concurrently (OPOSE_SCALE_STREAMS): the rate is the
-            # call's conv FLOPs over its wall latency, not over the (overlapping) launch times
+            # the four scales run in lockstep (one launch per layer covers every scale of the
+            # reference's loop, src/hand.py:36-57): the rate is the call's conv FLOPs over its wall latency,
+            # so the preprocessing, heat average and peak search count against it
             "conv_roofline": {"bound": "mfma", "achieved": flops / (ms * 1e-3) / 1e12, "peak": PEAK_CONV_TFLOPS,
                               "unit": "TFLOP/s", "frac": (flops / (ms * 1e-3) / 1e12) / PEAK_CONV_TFLOPS,
                               "basis": "conv FLOPs per call / host-to-host latency of the call"},

@@ -102,7 +102,7 @@ int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
 // OPOSE_PIPELINE_DEFER gate: the layer before which the next network records it ("stageN": before
 // CPM stage N).  Swept on the bench, same box: conv4_1 2,101, stage2 2,100, stage3 2,105, stage4
-// 2,107 frames/s against 2,110 with no gate (scripts/r4_gate_ab.sh, then with an env override)
+// 2,107 frames/s against 2,110 with no gate (a round-4 A/B, kept in git history)
 static const std::string& gate_layer() {
     static const std::string g = "conv3_1";
     return g;
@@ -526,7 +526,7 @@ TileChoice choose_tile(int Mpad, const std::vector<int>& gpix, int nK, bool x6 =
     // layers of one or two small frames (C2 / C3 / single-frame C5, stream-K over the whole chip):
     // 128x128 priced like the 8-wave tiles and 64x64 higher -- measured, C2 1.91 -> 1.72 ms and
     // Hand() 10.0 -> 9.9 ms, C5 and the bench unchanged; the same weights on the bench's
-    // 32-frame layers cost 6 % (scripts/c2_tile_ab.sh)
+    // 32-frame layers cost 6 % (a round-4 A/B, kept in git history)
     static const double ovh6_small[6] = {1.0, 1.0, 0.96, 1.1, 1.1, 1.6};
     const double* ovh6 = npix_all <= 16384 ? ovh6_small : ovh6_big;
     const double rate = x6 ? 0.4 : 1.0;

@@ -15,6 +15,7 @@ a single all_gather over xGMI (RCCL = torch.distributed 'nccl' on ROCm) per batc
 """
 from __future__ import annotations
 
+import datetime
 import functools
 import itertools
 
@@ -157,10 +158,15 @@ def _split_plan(costs, world, hls, trunk_frac, overhead):
     return best[1], best[2], best[3]
 
 
-def band_exchange(rank_up, rank_dn, group=None):
+def band_exchange(rank_up, rank_dn, group=None, timeout: float | None = None):
     """Halo exchange of one band for Body.band_maps: send_up -> the band above (rank_up), send_dn
     -> the band below (rank_dn), their rows into recv_up / recv_dn.  RCCL ('nccl'): device
-    P2P ops ordered on the library's stream; gloo: through host memory, synchronously."""
+    P2P ops ordered on the library's stream; gloo: through host memory, synchronously, each
+    send / recv waited for at most `timeout` seconds (None: the process group's own timeout), so
+    the neighbour of a rank that failed mid-band raises instead of blocking in its next exchange
+    (the library reports the callback's error as OPOSE_E_CALLBACK)."""
+    wait_kw = {} if timeout is None else {"timeout": datetime.timedelta(seconds=timeout)}
+
     def ex(xbuf, cap, n, stream):
         pairs = [(r, o) for r, o in ((rank_up, 0), (rank_dn, 1)) if r is not None]
         if dist.get_backend(group) == "nccl":
@@ -180,7 +186,7 @@ def band_exchange(rank_up, rank_dn, group=None):
             reqs.append(dist.isend(xbuf[o * cap:o * cap + n].cpu(), r, group=group))
             reqs.append(dist.irecv(recv[o], r, group=group))
         for q in reqs:
-            q.wait()
+            q.wait(**wait_kw)
         for _, o in pairs:
             xbuf[(2 + o) * cap:(2 + o) * cap + n].copy_(recv[o])
         if xbuf.is_cuda:
@@ -213,6 +219,12 @@ def abort_band_group(body, group=None, rccl: bool = False, destroy_group: bool =
             pass
 
 
+def abort_band(body, group, rccl: bool, abort_group):
+    """body_scale_sharded's failure path: abort_band_group, destroying a gloo group only for an
+    explicitly passed `group` unless the caller decides (abort_group)."""
+    abort_band_group(body, group, rccl, destroy_group=(group is not None) if abort_group is None else abort_group)
+
+
 def init_band_comm(body, group=None):
     """The library's own RCCL communicator over the ranks of `group` (Body.band_maps with
     exchange="rccl": halo send/recv on the library's stream, no Python between the layers).
@@ -243,12 +255,13 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
     §4.1), so a band's rows and a scale on another rank equal the one-GPU network's maps, and the
     post path is the same code.
     A band rank whose piece fails aborts its band communicator (RCCL) before re-raising; on the
-    RCCL path every band rank also waits for its exchanges for at most `band_timeout` seconds
-    (Handle.rccl_wait), so a neighbour of a failed rank aborts its own communicator and raises
-    TimeoutError instead of waiting forever.  gloo: a failing rank destroys the process group
-    (which releases its neighbours' pending send / recv) when `abort_group` is true; the default
-    is true only for an explicitly passed `group` -- the caller's WORLD group is left alone unless
-    asked.  KeyboardInterrupt / SystemExit are not band failures and abort nothing.
+    RCCL path every band rank, once all its pieces are enqueued, waits for its exchanges for at
+    most `band_timeout` seconds (one Handle.rccl_wait), so a neighbour of a failed rank aborts its
+    own communicator and raises TimeoutError instead of waiting forever.  gloo: each halo send /
+    recv is waited for at most `band_timeout` seconds, so the neighbours of a failed rank raise
+    too; the failing rank also destroys the process group (releasing the peers' pending send /
+    recv at once) when `abort_group` is true -- the default only for an explicitly passed
+    `group`: the caller's WORLD group is left alone unless asked.  KeyboardInterrupt / SystemExit are not band failures and abort nothing.
     maps_out: a list that receives the gathered per-scale maps on `dst` (tests)."""
     import numpy as np
     dev = hasattr(frame, "data_ptr")
@@ -274,6 +287,7 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
     if on_device and any(len(o) > 1 for o in owners):
         init_band_comm(body, group)  # collective: every rank, banded pieces or not
     pieces = {}  # (s, band) -> maps of this rank
+    banded = False
     for s in order:
         if rank not in owners[s]:
             continue
@@ -285,17 +299,24 @@ def body_scale_sharded(body, frame, rank: int, world: int, dst: int = 0, group=N
             up = owners[s][b - 1] if b > 0 else None
             dn = owners[s][b + 1] if b + 1 < len(owners[s]) else None
             try:
-                if on_device:  # RCCL: the library exchanges the halos itself
+                if on_device:  # RCCL: the library exchanges the halos itself, on its stream
                     body.handle.set_band_peers(up, dn)
                     m = body.band_maps(local[0], s, r0, r1, "rccl")
-                    body.handle.rccl_wait(band_timeout)  # a neighbour that failed: abort, raise
+                    banded = True
                 else:
-                    m = body.band_maps(local[0], s, r0, r1, band_exchange(up, dn, group))
+                    m = body.band_maps(local[0], s, r0, r1, band_exchange(up, dn, group, band_timeout))
             except Exception:
-                abort_band_group(body, group, on_device,
-                                 destroy_group=(group is not None) if abort_group is None else abort_group)
+                abort_band(body, group, on_device, abort_group)
                 raise
         pieces[(s, owners[s].index(rank))] = m if on_device else torch.from_numpy(m)
+    if banded:
+        # every piece is enqueued: one bounded wait for all of this rank's halo exchanges (a
+        # neighbour that failed -> the library aborts its communicator, TimeoutError here)
+        try:
+            body.handle.rccl_wait(band_timeout)
+        except Exception:
+            abort_band(body, group, on_device, abort_group)
+            raise
     maps = [None] * len(geoms)
     reqs = []
     for s in range(len(geoms)):

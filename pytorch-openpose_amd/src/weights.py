@@ -32,7 +32,7 @@ BENCH_OUT_SCALE = {
 # C5 (1080p, scale_search [0.5, 1, 1.5, 2]): the 368x656 calibration leaves most heat channels of
 # the averaged 1080p maps empty, so the heat conv gets its own per-channel affine, measured on
 # 1080p frames over the four scales' maps (scripts/calib_c5_stats.py: the 99.7th percentile of
-# each channel's pre-activations -> 0, its max -> 1; scripts/calib_c5_try.py: ~190 peaks and
+# each channel's pre-activations -> 0, its max -> 1; a one-off round-4 check: ~190 peaks and
 # ~10 assembled people per frame).  PAF as BENCH_OUT_SCALE.
 C5_OUT_SCALE = {
     "Mconv7_stage6_L2": (

@@ -27,6 +27,17 @@ def test_gpus_2_launches_two_ranks():
     assert d["n_gpus"] == 2 and d["frames_total"] == 2 * 4 * 2 and d["gathered_frames"] == 8
 
 
+def test_gpus_8_launches_eight_ranks():
+    """The driver's 8-GPU scaling run rehearsed: 8 gloo ranks x 32 frames, 256 records gathered
+    in frame order (dry_run asserts the order on every rank), one line from rank 0."""
+    out = _run(["--gpus", "8", "--dry-run", "--steps", "2", "--warmup", "1", "--batch", "32"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["gathered_frames"] == 256 and d["frames_total"] == 8 * 32 * 2
+
+
 def test_world_size_must_match_gpus():
     out = _run(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr

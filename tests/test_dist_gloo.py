@@ -316,7 +316,7 @@ class _FailingBandBody(_FakeBody):
         raise RuntimeError("band failed on this rank")
 
 
-def _failing_worker(rank, world, port, q, bad):
+def _failing_worker(rank, world, port, q, bad, abort_group=True, band_timeout=60.0):
     import sys
     for p in (PKG, REPO):
         if p not in sys.path:
@@ -327,7 +327,7 @@ def _failing_worker(rank, world, port, q, bad):
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=__import__("datetime").timedelta(seconds=600))
     try:
         body_scale_sharded(_FailingBandBody(rank == bad), np.zeros((90, 160, 3), np.uint8), rank, world, split="balanced",
-                           abort_group=True)
+                           abort_group=abort_group, band_timeout=band_timeout)
         q.put((rank, "returned"))
     except BaseException as e:  # noqa: BLE001 -- reported to the parent
         q.put((rank, "raised: %s" % type(e).__name__))
@@ -362,6 +362,35 @@ def test_failed_band_rank_does_not_hang_its_neighbours():
     assert res[bad] == "raised: RuntimeError", res
     for r in banded[1:]:
         assert res[r].startswith("raised"), res
+
+
+def test_failed_band_rank_gloo_bounded_wait_keeps_world_group():
+    """without abort_group the failing rank leaves the WORLD group alone, and its
+    neighbours still do not hang: each gloo halo send / recv waits at most band_timeout seconds
+    (band_exchange), so they raise in seconds, not after the group's 10-minute timeout."""
+    import sys
+    import time
+    sys.path.insert(0, PKG)
+    from src.dist import split_plan
+    world = 4
+    _, owners, _ = split_plan([g[0] * g[1] for g in GEOMS], world, [g[0] for g in GEOMS])
+    banded = [rs for rs in owners if len(rs) > 1][0]
+    bad = banded[0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29930 + os.getpid() % 16
+    t0 = time.time()
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, q, bad, False, 3.0)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert not p.is_alive()
+    assert res[bad] == "raised: RuntimeError", res
+    for r in banded[1:]:
+        assert res[r].startswith("raised"), res
+    assert time.time() - t0 < 100
 
 
 class _DeadlineHandle(_FakeHandle):
@@ -411,7 +440,8 @@ def test_rccl_band_neighbour_bounded_wait(monkeypatch, exc, aborts):
     with pytest.raises(type(exc)):
         sdist.body_scale_sharded(body, torch.zeros((90, 160, 3), dtype=torch.uint8), rank, world,
                                  band_timeout=0.25)
-    assert body.handle.waits == [0.25] and len(body.bands) == 1
+    # one bounded wait, after every banded piece of this rank was enqueued
+    assert body.handle.waits == [0.25] and len(body.bands) == sum(rank in rs for rs in owners if len(rs) > 1)
     assert body.handle.aborts == aborts and destroyed == []
 
 
