@@ -303,7 +303,7 @@ struct opose_ctx {
     }();
     // OPOSE_WINO=1: 3x3 layers that would run whole tiles on the window kernel run as Winograd
     // F(2,3) along x instead (conv_wino_x6, 2/3 of the MFMAs).  Opt-in: fp32-accurate and correct
-    // (tests/test_gpu_x6.py), but slower than the window kernel on this hardware (DESIGN §4.8)
+    // (tests/test_gpu_x6.py), but slower than the window kernel on this hardware (DESIGN §4.7)
     bool wino = [] {
         const char* e = getenv("OPOSE_WINO");
         return e && e[0] == '1';
