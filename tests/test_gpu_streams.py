@@ -74,6 +74,38 @@ def test_producer_on_the_handle_stream_then_pipelined(body):
     _same(body.decode_records(r2), exp)
 
 
+def test_signal_input_orders_the_next_upload(body):
+    """bench.py's host-to-host pattern (opose_signal_input): a pipelined call whose network is held
+    back (its input stream spins first), then the next batch written into the SAME frame buffer on
+    another stream ordered only by Handle.signal_input, then a second call on that stream.  The
+    overwrite must wait for the first call's network to have read the buffer: each call's records
+    are its own batch's."""
+    fx = np.random.default_rng(21).integers(0, 256, (2, 184, 328, 3), dtype=np.uint8)
+    fy = np.random.default_rng(22).integers(0, 256, (2, 184, 328, 3), dtype=np.uint8)
+    ex, ey = body.batch(fx), body.batch(fy)
+    sx, sy = torch.from_numpy(fx).cuda(), torch.from_numpy(fy).cuda()
+    dst = sx.clone()
+    rb = body.handle.record_bytes()
+    r1 = torch.empty((2, rb), dtype=torch.uint8, device="cuda")
+    r2 = torch.empty_like(r1)
+    for _ in range(2):  # the network stream exists; back-to-back pipelined calls
+        body.infer_records(dst, r1, pipeline=True)
+    body.handle.synchronize()
+    torch.cuda.synchronize()
+    side, up = torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(50_000_000)  # the first call's network starts only after this spin
+        body.infer_records(dst, r1, pipeline=True)
+    body.handle.signal_input(up)
+    with torch.cuda.stream(up):
+        dst.copy_(sy)  # must not land before the first network has read dst
+        body.infer_records(dst, r2, pipeline=True)
+    body.handle.synchronize()
+    torch.cuda.synchronize()
+    _same(body.decode_records(r1), ex)
+    _same(body.decode_records(r2), ey)
+
+
 def test_pipelined_multiscale_matches_serial():
     """Pipelined two-scale batches (each batch's scales run concurrently on per-scale streams
     forked from the network stream, its post-processing under the next batch's networks),
