@@ -470,7 +470,10 @@ def main():
     from src.dist import gather_records
 
     def step():
-        body.infer_records(frames, rec, pipeline="defer" if DEFER else PIPELINE)
+        # the frames are resident and complete, and only the handle's own stream touches rec (the
+        # gather below is queued on it): pipelined calls need no marker on torch's stream
+        # (wait=False, include/opose.h OPOSE_PIPELINE)
+        body.infer_records(frames, rec, pipeline="defer" if DEFER else PIPELINE, wait=not PIPELINE)
         if world > 1:
             # RCCL all_gather of the per-frame keypoint records, ordered after the library's
             # kernels on its stream (src/dist.py)

@@ -423,8 +423,10 @@ struct opose_ctx {
             event_pool.pop_back();
             return e;
         }
+        // timing-only events: no system-scope fence on record (no L2 writeback / invalidate
+        // between the bracketed launches; only hipEventElapsedTime reads them)
         hipEvent_t e;
-        OPOSE_HIP_CHECK(hipEventCreate(&e));
+        OPOSE_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         return e;
     }
     void prof_begin(ProfEntry& pe, const char* cls, double flops, double bytes) {
