@@ -195,3 +195,29 @@ def test_pipelined_stress_equals_serial(body, frames_np):
                         bad.append((k - 3 + j, f))
     assert not bad, "pipelined records differ from serial at (step, frame) %s" % bad[:10]
     assert sum(len(s) for _, s in ref[0]) > 10 * B  # crowded frames: the assembly is exercised
+
+
+def test_bench_loop_without_markers_equals_serial(body, frames_np):
+    """bench.py's timed loop exactly: the same resident frames and ONE records buffer every step,
+    pipelined calls with wait=False (no marker on torch's stream), each step's records copied out
+    on the handle's own stream (where the multi-rank gather is queued) -- 12 steps, every copy
+    equal to the serial records."""
+    d = torch.from_numpy(frames_np).cuda()
+    r = body.infer_records(d)
+    body.handle.synchronize()
+    ref = body.decode_records(r)
+    rb = body.handle.record_bytes()
+    rec = torch.empty((B, rb), dtype=torch.uint8, device=d.device)
+    outs = [torch.empty_like(rec) for _ in range(12)]
+    torch.cuda.synchronize()
+    lib = body.handle.torch_stream()
+    for k in range(12):
+        body.infer_records(d, rec, pipeline=True, wait=False)
+        with torch.cuda.stream(lib):
+            outs[k].copy_(rec)
+    body.handle.synchronize()
+    torch.cuda.synchronize()
+    bad = [(k, f) for k in range(12)
+           for f, ((c, s), (rc, rs)) in enumerate(zip(body.decode_records(outs[k]), ref))
+           if not (np.array_equal(c, rc) and np.array_equal(s, rs))]
+    assert not bad, "records differ from serial at (step, frame) %s" % bad[:10]
